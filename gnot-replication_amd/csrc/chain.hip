@@ -1,0 +1,237 @@
+// Fused MLP chains (reference MLP, model.py:5-18) — forward and backward.
+//
+// One wave carries 16 points through ALL nl+1 Linears of one MLP with the activations resident in
+// VGPRs (point form, gnot_common.h): Linear -> +bias -> exact-erf GELU -> next Linear ... The
+// MFMA output of a layer is directly the B operand of the next one, so a chain touches HBM only
+// for its input rows, its output rows and (training) the saved pre-activations.  grid.y selects
+// the chain, which is how the E experts of a soft-MoE (model.py:123-137) run side by side on the
+// same input; the three epilogues cover every MLP of GNOT:
+//   CH_STORE   plain output (x / input-function encoders, decoder: model.py:146, 149, 152)
+//   CH_SOFTMAX softmax over the outputs (gating over experts, model.py:148, 155-156)
+//   CH_MOE     expert output scaled by its per-point gate weight into a per-expert stage
+//              (model.py:128-130; the residual add + sum over experts is moe_combine / the consumer)
+// The backward kernel walks the same chain in reverse with the transposed weight images,
+// re-applying GELU'(saved pre-activation), and writes each layer's dZ for the weight-gradient pass.
+#include "gnot_common.h"
+#include "gnot_kernels.h"
+
+namespace gnot {
+
+template <int D, int KT0, int OTL>
+__global__ void __launch_bounds__(256) chain_fwd_kernel(ChainArgs a) {
+  constexpr int DT = D / 16;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const long p = ((long)blockIdx.x * 4 + wave) * 16 + (lane & 15);
+  const bool valid = p < a.P;
+  const int e = blockIdx.y;
+  const ChainLayer* L = a.layers + e * a.nlin;
+  float* save = a.save ? a.save + e * a.save_chain_stride : nullptr;
+
+  float h[DT][4];
+  {
+    float x0[KT0][4];
+    load_rows<KT0>(x0, a.X, a.ldx, p, valid, a.in_dim, lane);
+    f32x4 acc[DT];
+    init_bias<DT>(acc, L[0].bias, lane);
+    mm_tiles<KT0, DT>(L[0].Wp, x0, acc, lane);
+    acc_to_regs<DT>(acc, h);
+  }
+  if (save) store_rows<DT>(h, save, D, p, valid, D, lane);
+#pragma unroll
+  for (int T = 0; T < DT; ++T)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) h[T][r] = gelu(h[T][r]);
+
+  for (int l = 1; l < a.nlin - 1; ++l) {
+    f32x4 acc[DT];
+    init_bias<DT>(acc, L[l].bias, lane);
+    mm_tiles<DT, DT>(L[l].Wp, h, acc, lane);
+    acc_to_regs<DT>(acc, h);
+    if (save) store_rows<DT>(h, save + l * a.save_layer_stride, D, p, valid, D, lane);
+#pragma unroll
+    for (int T = 0; T < DT; ++T)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) h[T][r] = gelu(h[T][r]);
+  }
+
+  float y[OTL][4];
+  {
+    f32x4 acc[OTL];
+    init_bias<OTL>(acc, L[a.nlin - 1].bias, lane);
+    mm_tiles<DT, OTL>(L[a.nlin - 1].Wp, h, acc, lane);
+    acc_to_regs<OTL>(acc, y);
+  }
+  if (save) store_rows<OTL>(y, save + (a.nlin - 1) * a.save_layer_stride, D, p, valid, 16 * OTL, lane);
+
+  const int g = lane >> 4;
+  if (a.mode == CH_SOFTMAX) {
+    // softmax over the first out_dim outputs (features 16T + 4g + r); padded features excluded
+    float m = -INFINITY;
+#pragma unroll
+    for (int T = 0; T < OTL; ++T)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (16 * T + 4 * g + r < a.out_dim) m = fmaxf(m, y[T][r]);
+    m = fmaxf(m, shfl_xor(m, 16));
+    m = fmaxf(m, shfl_xor(m, 32));
+    float sum = 0.f;
+#pragma unroll
+    for (int T = 0; T < OTL; ++T)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool in = 16 * T + 4 * g + r < a.out_dim;
+        y[T][r] = in ? __expf(y[T][r] - m) : 0.f;
+        sum += y[T][r];
+      }
+    sum += shfl_xor(sum, 16);
+    sum += shfl_xor(sum, 32);
+    const float inv = 1.0f / sum;
+#pragma unroll
+    for (int T = 0; T < OTL; ++T)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) y[T][r] *= inv;
+    store_rows<OTL>(y, a.Y + e * a.y_chain_stride, a.ldy, p, valid, a.out_dim, lane);
+  } else if (a.mode == CH_MOE) {
+    const float s = valid ? a.scores[p * a.ldsc + e] : 0.f;
+#pragma unroll
+    for (int T = 0; T < OTL; ++T)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) y[T][r] *= s;
+    store_rows<OTL>(y, a.Y + e * a.y_chain_stride, a.ldy, p, valid, a.out_dim, lane);
+  } else {
+    store_rows<OTL>(y, a.Y + e * a.y_chain_stride, a.ldy, p, valid, a.out_dim, lane);
+  }
+}
+
+template <int D, int KT0, int OTL>
+__global__ void __launch_bounds__(256) chain_bwd_kernel(ChainArgs a) {
+  constexpr int DT = D / 16;
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4;
+  const int wave = threadIdx.x >> 6;
+  const long p = ((long)blockIdx.x * 4 + wave) * 16 + (lane & 15);
+  const bool valid = p < a.P;
+  const int e = blockIdx.y;
+  const ChainLayer* L = a.layers + e * a.nlin;
+  const float* save = a.save + e * a.save_chain_stride;
+  float* dz = a.dz ? a.dz + e * a.dz_chain_stride : nullptr;
+
+  // ---- gradient at the chain output
+  float dy[OTL][4];
+  if (a.mode == CH_MOE) {
+    // query_out = query_in + sum_e s_e * y_e : dy_e = s_e * dq ; ds_e = dq . y_e (model.py:128-131)
+    float yv[OTL][4];
+    load_rows<OTL>(dy, a.dY, a.lddy, p, valid, 16 * OTL, lane);
+    load_rows<OTL>(yv, save + (a.nlin - 1) * a.save_layer_stride, D, p, valid, 16 * OTL, lane);
+    float ds = 0.f;
+#pragma unroll
+    for (int T = 0; T < OTL; ++T)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ds += dy[T][r] * yv[T][r];
+    ds += shfl_xor(ds, 16);
+    ds += shfl_xor(ds, 32);
+    const float s = valid ? a.scores[p * a.ldsc + e] : 0.f;
+    if (valid && g == 0) a.dscore[p * a.ldsc + e] += ds;
+#pragma unroll
+    for (int T = 0; T < OTL; ++T)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dy[T][r] *= s;
+  } else if (a.mode == CH_SOFTMAX) {
+    // d logits = s * (ds - <s, ds>)   (softmax over experts, model.py:156)
+    float sv[OTL][4];
+    load_rows<OTL>(sv, a.scores, a.ldsc, p, valid, a.out_dim, lane);
+    load_rows<OTL>(dy, a.dscore, a.ldsc, p, valid, a.out_dim, lane);
+    float dot = 0.f;
+#pragma unroll
+    for (int T = 0; T < OTL; ++T)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dot += sv[T][r] * dy[T][r];
+    dot += shfl_xor(dot, 16);
+    dot += shfl_xor(dot, 32);
+#pragma unroll
+    for (int T = 0; T < OTL; ++T)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dy[T][r] = sv[T][r] * (dy[T][r] - dot);
+  } else {
+    load_rows<OTL>(dy, a.dY, a.lddy, p, valid, a.out_dim, lane);
+  }
+
+  // ---- last Linear
+  if (dz) store_rows<OTL>(dy, dz + (a.nlin - 1) * a.dz_layer_stride, D, p, valid, 16 * OTL, lane);
+  float gr[DT][4];
+  {
+    f32x4 acc[DT];
+    init_bias<DT>(acc, nullptr, lane);
+    mm_tiles<OTL, DT>(L[a.nlin - 1].WpT, dy, acc, lane);
+    acc_to_regs<DT>(acc, gr);
+  }
+  // ---- hidden Linears, reverse
+  for (int l = a.nlin - 2; l >= 1; --l) {
+    float hs[DT][4];
+    load_rows<DT>(hs, save + l * a.save_layer_stride, D, p, valid, D, lane);
+#pragma unroll
+    for (int T = 0; T < DT; ++T)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) gr[T][r] *= gelu_grad(hs[T][r]);
+    if (dz) store_rows<DT>(gr, dz + l * a.dz_layer_stride, D, p, valid, D, lane);
+    f32x4 acc[DT];
+    init_bias<DT>(acc, nullptr, lane);
+    mm_tiles<DT, DT>(L[l].WpT, gr, acc, lane);
+    acc_to_regs<DT>(acc, gr);
+  }
+  // ---- first Linear
+  {
+    float hs[DT][4];
+    load_rows<DT>(hs, save, D, p, valid, D, lane);
+#pragma unroll
+    for (int T = 0; T < DT; ++T)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) gr[T][r] *= gelu_grad(hs[T][r]);
+    if (dz) store_rows<DT>(gr, dz, D, p, valid, D, lane);
+  }
+  if (a.dX) {
+    f32x4 acc[KT0];
+    init_bias<KT0>(acc, nullptr, lane);
+    mm_tiles<DT, KT0>(L[0].WpT, gr, acc, lane);
+    float dx[KT0][4];
+    acc_to_regs<KT0>(acc, dx);
+    store_rows<KT0>(dx, a.dX + e * a.dx_chain_stride, a.lddx, p, valid, a.in_dim, lane);
+  }
+}
+
+template <int D>
+static hipError_t launch_chain_d(const ChainArgs& a, bool bwd, hipStream_t s) {
+  constexpr int DT = D / 16;
+  const dim3 grid((a.P + 63) / 64, a.nchains), block(256);
+#define GNOT_CHAIN_CASE(K0, OL)                                                              \
+  if (a.KT0 == K0 && a.OTL == OL) {                                                           \
+    if (bwd) hipLaunchKernelGGL((chain_bwd_kernel<D, K0, OL>), grid, block, 0, s, a);          \
+    else hipLaunchKernelGGL((chain_fwd_kernel<D, K0, OL>), grid, block, 0, s, a);              \
+    return hipGetLastError();                                                                 \
+  }
+  GNOT_CHAIN_CASE(1, 1)
+  GNOT_CHAIN_CASE(1, DT)
+  GNOT_CHAIN_CASE(DT, 1)
+  GNOT_CHAIN_CASE(DT, DT)
+#undef GNOT_CHAIN_CASE
+  return hipErrorInvalidValue;
+}
+
+static hipError_t launch_chain(const ChainArgs& a, bool bwd, hipStream_t s) {
+  if (a.P <= 0 || a.nchains <= 0) return hipSuccess;
+  if (a.nlin < 2) return hipErrorInvalidValue;
+  switch (a.D) {
+    case 32: return launch_chain_d<32>(a, bwd, s);
+    case 48: return launch_chain_d<48>(a, bwd, s);
+    case 64: return launch_chain_d<64>(a, bwd, s);
+    case 128: return launch_chain_d<128>(a, bwd, s);
+    case 256: return launch_chain_d<256>(a, bwd, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t launch_chain_fwd(const ChainArgs& a, hipStream_t s) { return launch_chain(a, false, s); }
+hipError_t launch_chain_bwd(const ChainArgs& a, hipStream_t s) { return launch_chain(a, true, s); }
+
+}  // namespace gnot

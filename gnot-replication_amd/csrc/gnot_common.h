@@ -1,0 +1,186 @@
+// Shared device helpers for the GNOT MI355X (gfx950) kernels.
+//
+// Register "point form" used by every point-streaming kernel in this library
+// ---------------------------------------------------------------------------
+// A wave owns 16 consecutive points (rows of a [P, F] row-major activation).  Lane l holds
+// point  p0 + (l & 15)  and, for every 16-feature tile T, the four features
+//            16*T + 4*(l >> 4) + r ,  r = 0..3      ->  act[T][r]
+// This is exactly the C/D layout of v_mfma_f32_16x16x4_f32 when the MFMA computes
+// OUT^T = W * ACT^T (output features on MFMA rows, points on MFMA columns), and it is also the
+// B-operand layout that the next 16x16x4 MFMA needs when it contracts over those features:
+// B[k = l>>4][j = l&15] at k-step r is feature 16T + 4(l>>4) + r of point j.  A whole MLP chain
+// therefore runs with activations resident in VGPRs, no LDS transpose between layers; only the
+// weights (A operand) are streamed, from a pre-packed "fragment order" image (pack.hip) in which
+// one wave-instruction reads 1 KiB contiguous (16 B per lane).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define GNOT_DEV __device__ __forceinline__
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+namespace gnot {
+
+constexpr int WAVE = 64;
+
+// one k=4 step of the f32-input MFMA: acc(16x16) += A(16x4) * B(4x16)
+GNOT_DEV f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// acc += W-fragment (float4 = 4 k-steps) x act tile (4 regs)
+GNOT_DEV f32x4 mfma_k16(const float4 w, const float (&x)[4], f32x4 c) {
+  c = mfma4(w.x, x[0], c);
+  c = mfma4(w.y, x[1], c);
+  c = mfma4(w.z, x[2], c);
+  c = mfma4(w.w, x[3], c);
+  return c;
+}
+
+constexpr float kSqrt1_2 = 0.70710678118654752440f;
+constexpr float kInvSqrt2Pi = 0.39894228040143267794f;
+
+// nn.GELU() (exact erf), reference model.py:10,13
+GNOT_DEV float gelu(float x) { return 0.5f * x * (1.0f + erff(x * kSqrt1_2)); }
+GNOT_DEV float gelu_grad(float x) {
+  return 0.5f * (1.0f + erff(x * kSqrt1_2)) + x * kInvSqrt2Pi * __expf(-0.5f * x * x);
+}
+
+GNOT_DEV float shfl_xor(float v, int m) { return __shfl_xor(v, m, 64); }
+
+// ---- point-form loads / stores ------------------------------------------------------------
+// load KT tiles of row p (features 16T + 4g + r); features >= ncols read as 0; invalid rows -> 0
+// (16-byte loads when the row pitch allows it; X must then be 16-byte aligned)
+template <int KT>
+GNOT_DEV void load_rows(float (&a)[KT][4], const float* __restrict__ X, long ld, long p, bool valid,
+                        int ncols, int lane) {
+  const int g = lane >> 4;
+#pragma unroll
+  for (int T = 0; T < KT; ++T) {
+    const int f = 16 * T + 4 * g;
+    if (valid && f + 3 < ncols && (ld & 3) == 0) {
+      const float4 v = *reinterpret_cast<const float4*>(X + p * ld + f);
+      a[T][0] = v.x; a[T][1] = v.y; a[T][2] = v.z; a[T][3] = v.w;
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) a[T][r] = (valid && f + r < ncols) ? X[p * ld + f + r] : 0.f;
+    }
+  }
+}
+
+template <int KT>
+GNOT_DEV void store_rows(const float (&a)[KT][4], float* __restrict__ Y, long ld, long p, bool valid,
+                         int ncols, int lane) {
+  if (!valid) return;
+  const int g = lane >> 4;
+#pragma unroll
+  for (int T = 0; T < KT; ++T) {
+    const int f = 16 * T + 4 * g;
+    if (f + 3 < ncols && (ld & 3) == 0) {
+      *reinterpret_cast<float4*>(Y + p * ld + f) = make_float4(a[T][0], a[T][1], a[T][2], a[T][3]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (f + r < ncols) Y[p * ld + f + r] = a[T][r];
+    }
+  }
+}
+
+// OUT^T(16*OT x 16 points) = W(16*OT x 16*KT) * IN^T with W given in packed fragment order:
+// Wp[(o*KT + T)*64 + lane] = { W[16o + (lane&15)][16T + 4(lane>>4) + r] : r = 0..3 }
+// acc must be pre-initialised (bias or zero).
+template <int KT, int OT>
+GNOT_DEV void mm_tiles(const float4* __restrict__ Wp, const float (&in)[KT][4], f32x4 (&acc)[OT],
+                       int lane) {
+#pragma unroll
+  for (int T = 0; T < KT; ++T) {
+    float4 w[OT];
+#pragma unroll
+    for (int o = 0; o < OT; ++o) w[o] = Wp[(o * KT + T) * WAVE + lane];
+#pragma unroll
+    for (int o = 0; o < OT; ++o) acc[o] = mfma_k16(w[o], in[T], acc[o]);
+  }
+}
+
+template <int OT>
+GNOT_DEV void init_bias(f32x4 (&acc)[OT], const float* __restrict__ bias, int lane) {
+  const int g = lane >> 4;
+#pragma unroll
+  for (int o = 0; o < OT; ++o) {
+    if (bias) {
+      const float4 b = *reinterpret_cast<const float4*>(bias + 16 * o + 4 * g);
+      acc[o] = f32x4{b.x, b.y, b.z, b.w};
+    } else {
+      acc[o] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+}
+
+template <int OT>
+GNOT_DEV void acc_to_regs(const f32x4 (&acc)[OT], float (&h)[OT][4]) {
+#pragma unroll
+  for (int o = 0; o < OT; ++o) {
+    h[o][0] = acc[o][0]; h[o][1] = acc[o][1]; h[o][2] = acc[o][2]; h[o][3] = acc[o][3];
+  }
+}
+
+// Feature softmax over heads of `dh` consecutive features (model.py:59, 72, 93) applied to the
+// point-form tile set h[OT][4] (features 16T + 4g + r).  Supported: dh = 4, 8 or a multiple of 16.
+template <int OT>
+GNOT_DEV void softmax_heads(float (&h)[OT][4], int dh) {
+  if (dh == 4) {
+#pragma unroll
+    for (int T = 0; T < OT; ++T) {
+      float m = fmaxf(fmaxf(h[T][0], h[T][1]), fmaxf(h[T][2], h[T][3]));
+      float s = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { h[T][r] = __expf(h[T][r] - m); s += h[T][r]; }
+      const float inv = 1.0f / s;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) h[T][r] *= inv;
+    }
+  } else if (dh == 8) {
+#pragma unroll
+    for (int T = 0; T < OT; ++T) {
+      float m = fmaxf(fmaxf(h[T][0], h[T][1]), fmaxf(h[T][2], h[T][3]));
+      m = fmaxf(m, shfl_xor(m, 16));
+      float s = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { h[T][r] = __expf(h[T][r] - m); s += h[T][r]; }
+      s += shfl_xor(s, 16);
+      const float inv = 1.0f / s;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) h[T][r] *= inv;
+    }
+  } else {
+    const int tph = dh >> 4;  // tiles per head
+    for (int T0 = 0; T0 < OT; T0 += tph) {
+      float m = -INFINITY;
+#pragma unroll
+      for (int T = 0; T < OT; ++T)
+        if (T >= T0 && T < T0 + tph)
+          m = fmaxf(m, fmaxf(fmaxf(h[T][0], h[T][1]), fmaxf(h[T][2], h[T][3])));
+      m = fmaxf(m, shfl_xor(m, 16));
+      m = fmaxf(m, shfl_xor(m, 32));
+      float s = 0.f;
+#pragma unroll
+      for (int T = 0; T < OT; ++T)
+        if (T >= T0 && T < T0 + tph) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) { h[T][r] = __expf(h[T][r] - m); s += h[T][r]; }
+        }
+      s += shfl_xor(s, 16);
+      s += shfl_xor(s, 32);
+      const float inv = 1.0f / s;
+#pragma unroll
+      for (int T = 0; T < OT; ++T)
+        if (T >= T0 && T < T0 + tph) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) h[T][r] *= inv;
+        }
+    }
+  }
+}
+
+}  // namespace gnot

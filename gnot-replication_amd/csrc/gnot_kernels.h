@@ -1,0 +1,144 @@
+// Internal (C++) launcher interface between the engine and the HIP kernels.
+// The public C-ABI lives in include/gnot_hip.h; nothing here crosses the library boundary.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gnot {
+
+// ------------------------------------------------------------------ weight packing (pack.hip)
+// One Linear (W [out, in] row-major, bias [out]) written into the fragment-order image used as the
+// MFMA A operand (see gnot_common.h).  transposed=0: A = W   (forward, out = x W^T + b)
+//                                       transposed=1: A = W^T (backward data, dx = dy W)
+// Tile (o, T) of this matrix lands at dst[((o0 + o) * ktot + t0 + T) * 64 + lane] (float4 units), so
+// several Linears can be concatenated along either dimension of one packed matrix.
+struct PackJob {
+  const float* W;
+  const float* b;      // may be null; only used when bias_dst != null
+  float4* dst;
+  float* bias_dst;     // padded bias copy (16*OTp floats, zero filled), or null
+  int out, in;
+  int transposed;
+  int o0, t0, ktot;
+  int OTp, KTp;        // tile counts of this job's image (>= what out/in need; the rest is zero)
+};
+hipError_t launch_pack(const PackJob* jobs_dev, const int* tile_prefix_dev, int njobs,
+                       int total_tiles, hipStream_t s);
+
+// ------------------------------------------------------------------ projections (linear.hip)
+enum LinearEpi { EPI_STORE = 0, EPI_ACCUM = 1 };
+struct LinearArgs {
+  const float* X;      // input rows: sum_{s<nsum} X[s*sum_stride + p*ldx + f]
+  long ldx;
+  int nsum;
+  long sum_stride;
+  int K;               // real input columns (<= 16*KT)
+  const float4* Wp;    // packed A operand, KT = ceil(K/16) tiles per output tile
+  const float* bias;   // padded bias or null
+  float* Y;
+  long ldy;
+  int NO;              // output columns (multiple of 16)
+  int P;               // rows
+  int epi;             // LinearEpi
+  int nsoft;           // feature-softmax on output columns [0, nsoft)
+  int dh;              // head width for that softmax
+};
+hipError_t launch_linear(const LinearArgs& a, int D, hipStream_t s);   // K <= D, NO % D == 0
+
+// ------------------------------------------------------------------ fused MLP chains (chain.hip)
+enum ChainMode { CH_STORE = 0, CH_SOFTMAX = 1, CH_MOE = 2 };
+struct ChainLayer {
+  const float4* Wp;    // packed forward weights of this layer
+  const float4* WpT;   // packed transposed weights (backward)
+  const float* bias;   // padded bias
+};
+struct ChainArgs {
+  int D;               // hidden width
+  int KT0, OTL;        // input / last-output tile counts (1 or D/16)
+  int nlin;            // number of Linears (>= 2)
+  int in_dim, out_dim;
+  int P;
+  int nchains;         // grid.y
+  const ChainLayer* layers;          // device table [nchains * nlin]
+  // forward
+  const float* X; long ldx;          // chain input (shared by all chains)
+  float* Y; long ldy; long y_chain_stride;   // output (CH_STORE/CH_SOFTMAX) or MoE stage
+  const float* scores; int ldsc;     // CH_MOE: expert weights scores[p*ldsc + chain]; CH_SOFTMAX bwd: s
+  int mode;
+  float* save; long save_layer_stride; long save_chain_stride;  // pre-activations [P, D] per layer (ld D)
+  // backward
+  const float* dY; long lddy;        // incoming grad (CH_STORE: [P,out]; CH_MOE: dquery [P,D]);
+  float* dscore;                     // CH_MOE: dscore[p*ldsc + chain] += dq . y ; CH_SOFTMAX: d(scores)
+  float* dz; long dz_layer_stride; long dz_chain_stride;          // per layer dZ [P, D] for wgrad
+  float* dX; long lddx; long dx_chain_stride;                     // chain input grad or null
+};
+hipError_t launch_chain_fwd(const ChainArgs& a, hipStream_t s);
+hipError_t launch_chain_bwd(const ChainArgs& a, hipStream_t s);
+
+// ------------------------------------------------------------------ weight gradients (wgrad.hip)
+struct WgradJob {
+  const float* dz; long lddz;        // [P, out]   (columns [0, out))
+  const float* x;  long ldx;         // [P, in]
+  int x_gelu;                        // 1: the layer input is gelu(x)
+  int out, in;
+  float* dW;                         // [out, in] row-major (parameter gradient layout)
+  float* db;                         // [out] or null
+  int P;
+  int tiles_o, tiles_i;              // 32x32 output tiles
+  int splits;                        // split-K count over points
+  long slab_off;                     // offset (floats) of this job's partial slabs in the workspace
+  int accumulate;                    // 1: dW += result
+};
+hipError_t launch_wgrad(const WgradJob* jobs_dev, const int* wave_prefix_dev, int njobs, int total_waves,
+                        const int* red_prefix_dev, int total_red, float* slab, hipStream_t s);
+
+// ------------------------------------------------------------------ attention (attn.hip)
+struct Segment { int b; int start; int len; int chunk0; };   // one point chunk of one sample
+struct AttnStateArgs {
+  const float* A; long lda;          // [P, d] (head h at columns h*dh)
+  const float* Bv; long ldb;
+  const float* w; long ldw;          // optional [P, H] weights for z (null -> 1)
+  int H, dh;
+  const int4* chunks;                // (b, start, len, -) per chunk
+  int nchunks;
+  float* slab;                       // [nchunks][H][dh*dh + dh]
+  const int* sample_chunk_off;       // [B+1] chunk ranges per sample
+  int B;
+  float* state;                      // [B][H][dh*dh + dh]
+};
+hipError_t launch_attn_state(const AttnStateArgs& a, hipStream_t s);
+
+struct AttnApplyArgs {
+  const float* q; long ldq;          // post-softmax q, point-major
+  int nsrc;                          // number of (S, z) sets to average (I, or 1 for self)
+  const float* state[8];             // [B][H][dh*dh + dh] per source
+  const int4* chunks; int nchunks;
+  const long* off;                   // [B+1] sample offsets (device)
+  int H, dh;
+  float* res;                        // [P, d] head-major per sample (the scramble)
+  // backward
+  const float* dres;                 // [P, d] head-major per sample
+  float* dq_pre; long lddq;          // grad wrt pre-softmax q, point-major
+  float* du[8]; long lddu;           // per source du, point-major
+  float* dden[8];                    // per source [P, H]
+};
+hipError_t launch_attn_apply_fwd(const AttnApplyArgs& a, hipStream_t s);
+hipError_t launch_attn_apply_bwd(const AttnApplyArgs& a, hipStream_t s);
+
+struct AttnKVBwdArgs {
+  const float* k; const float* v; long ldkv;   // post-softmax k, v (point-major)
+  const float* dstate;               // [B][H][dh*dh + dh]  (dS, dz)
+  const int4* chunks; int nchunks;
+  int H, dh;
+  float* dk; float* dv; long lddkv;  // pre-softmax dK, dV
+};
+hipError_t launch_attn_kv_bwd(const AttnKVBwdArgs& a, hipStream_t s);
+
+// ------------------------------------------------------------------ small elementwise (misc.hip)
+hipError_t launch_concat_theta(const float* x, long ldx, int in_dim, const float* theta, int th_dim,
+                               const long* off, int B, float* xin, long ldxin, int P, hipStream_t s);
+// out = (base ? base : 0) + sum_e stage[e]
+hipError_t launch_moe_combine(const float* base, const float* stage, long stage_stride, int E,
+                              float* out, long n, hipStream_t s);
+
+}  // namespace gnot

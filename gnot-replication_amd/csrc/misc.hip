@@ -1,0 +1,68 @@
+// Small point-streaming kernels around the hot path.
+//   concat_theta : x_in[p] = cat(x[p], theta[sample(p)])   (reference model.py:158-159; theta is
+//                  broadcast per sample over that sample's points — packed offsets, no padding)
+//   moe_combine  : q_out = q_in + sum_e stage[e]           (reference model.py:129-131, 135-137)
+//                  (q_in may be null: plain sum, used for the expert-summed dX of the MoE backward)
+#include "gnot_common.h"
+#include "gnot_kernels.h"
+
+namespace gnot {
+
+__global__ void __launch_bounds__(256) concat_theta_kernel(const float* __restrict__ x, long ldx, int in_dim,
+                                                           const float* __restrict__ theta, int th_dim,
+                                                           const long* __restrict__ off, int B,
+                                                           float* __restrict__ xin, long ldxin, int P) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)P * ldxin) return;
+  const long p = i / ldxin;
+  const int c = (int)(i % ldxin);
+  float v = 0.f;                                   // pad columns are zero
+  if (c < in_dim) {
+    v = x[p * ldx + c];
+  } else if (c < in_dim + th_dim) {
+    int lo = 0, hi = B - 1;                        // sample of point p
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (off[mid] <= p) lo = mid; else hi = mid - 1;
+    }
+    v = theta[(long)lo * th_dim + (c - in_dim)];
+  }
+  xin[i] = v;
+}
+
+hipError_t launch_concat_theta(const float* x, long ldx, int in_dim, const float* theta, int th_dim,
+                               const long* off, int B, float* xin, long ldxin, int P, hipStream_t s) {
+  const long n = (long)P * ldxin;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(concat_theta_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, ldx, in_dim,
+                     theta, th_dim, off, B, xin, ldxin, P);
+  return hipGetLastError();
+}
+
+__global__ void __launch_bounds__(256) moe_combine_kernel(const float4* __restrict__ base,
+                                                          const float4* __restrict__ stage,
+                                                          long stage_stride4, int E,
+                                                          float4* __restrict__ out, long n4) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+    float4 v = base ? base[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int e = 0; e < E; ++e) {
+      const float4 s = stage[e * stage_stride4 + i];
+      v.x += s.x; v.y += s.y; v.z += s.z; v.w += s.w;
+    }
+    out[i] = v;
+  }
+}
+
+hipError_t launch_moe_combine(const float* base, const float* stage, long stage_stride, int E,
+                              float* out, long n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if ((n & 3) || (stage_stride & 3)) return hipErrorInvalidValue;
+  const long n4 = n / 4;
+  const long blocks = std::min<long>((n4 + 255) / 256, 4096);
+  hipLaunchKernelGGL(moe_combine_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
+                     reinterpret_cast<const float4*>(base), reinterpret_cast<const float4*>(stage),
+                     stage_stride / 4, E, reinterpret_cast<float4*>(out), n4);
+  return hipGetLastError();
+}
+
+}  // namespace gnot

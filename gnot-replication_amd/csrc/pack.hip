@@ -1,0 +1,64 @@
+// Weight packing: nn.Linear weights -> MFMA A-operand fragment-order images.
+//
+// Every Linear of the model (reference model.py:9-14, 43-51) is re-laid out once per step (after
+// the optimizer touched the parameters) into two images:
+//   forward  A = W   : lane l of tile (o, T) holds W[16o + (l&15)][16T + 4(l>>4) + 0..3]
+//   backward A = W^T : lane l of tile (o, T) holds W[16T + 4(l>>4) + 0..3][16o + (l&15)]
+// so that a kernel's A-operand read is one contiguous 1 KiB wave-instruction (16 B per lane).
+// Out-of-range rows/columns are written as zeros, which is what lets the chain/linear kernels run
+// every layer on whole 16-wide tiles (odd in/out widths such as input_dim+theta_dim = 3 or
+// n_expert = 3 cost nothing but padding).
+#include "gnot_common.h"
+#include "gnot_kernels.h"
+
+namespace gnot {
+
+// one wave per (job, tile)
+__global__ void __launch_bounds__(64) pack_kernel(const PackJob* __restrict__ jobs,
+                                                  const int* __restrict__ prefix, int njobs) {
+  const int tile_id = blockIdx.x;
+  // binary search: last job with prefix[j] <= tile_id
+  int lo = 0, hi = njobs - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (prefix[mid] <= tile_id) lo = mid; else hi = mid - 1;
+  }
+  const PackJob& J = jobs[lo];
+  const int t = tile_id - prefix[lo];
+  const int lane = threadIdx.x;
+  const int r16 = lane & 15, g = lane >> 4;
+  float v[4];
+  int o, T;
+  if (!J.transposed) {
+    o = t / J.KTp; T = t % J.KTp;
+    const int row = 16 * o + r16;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int col = 16 * T + 4 * g + r;
+      v[r] = (row < J.out && col < J.in) ? J.W[(long)row * J.in + col] : 0.f;
+    }
+  } else {                              // contraction runs over W's rows
+    o = t / J.KTp; T = t % J.KTp;
+    const int col = 16 * o + r16;       // W column (input feature)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * T + 4 * g + r;
+      v[r] = (row < J.out && col < J.in) ? J.W[(long)row * J.in + col] : 0.f;
+    }
+  }
+  J.dst[((long)(J.o0 + o) * J.ktot + J.t0 + T) * WAVE + lane] = make_float4(v[0], v[1], v[2], v[3]);
+  // padded bias copy, done by the job's first tile
+  if (J.bias_dst && t == 0) {
+    const int nb = 16 * J.OTp;
+    for (int i = lane; i < nb; i += WAVE) J.bias_dst[i] = (i < J.out && J.b) ? J.b[i] : 0.f;
+  }
+}
+
+hipError_t launch_pack(const PackJob* jobs_dev, const int* tile_prefix_dev, int njobs,
+                       int total_tiles, hipStream_t s) {
+  if (total_tiles <= 0) return hipSuccess;
+  hipLaunchKernelGGL(pack_kernel, dim3(total_tiles), dim3(64), 0, s, jobs_dev, tile_prefix_dev, njobs);
+  return hipGetLastError();
+}
+
+}  // namespace gnot

@@ -1,0 +1,83 @@
+"""ctypes binding of libgnot_hip.so (C ABI: include/gnot_hip.h).
+
+This is the reference-side binding a maintainer adds to aloe101/GNOT-Replication (see
+INTEGRATION.md): plain pointers and sizes, one `gnot_plan` per model.  There is deliberately no
+fallback: if the shared library is missing or cannot be loaded, importing the product path fails.
+"""
+import ctypes
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(_HERE)                      # gnot-replication_amd/
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libgnot_hip.so")
+CSRC = os.path.join(PKG_ROOT, "csrc")
+
+
+class GnotConfig(ctypes.Structure):
+    """gnot_config: the 12 GNOT constructor arguments (reference model.py:143)."""
+    _fields_ = [(n, ctypes.c_int) for n in (
+        "input_dim", "theta_dim", "input_func_dim", "out_dim", "n_attn_layers", "n_attn_hidden_dim",
+        "n_mlp_num_layers", "n_mlp_hidden_dim", "n_input_hidden_dim", "n_expert", "n_head",
+        "n_input_functions")]
+
+
+EXPORTS = [
+    "gnot_plan_create", "gnot_plan_destroy", "gnot_plan_num_linears", "gnot_plan_linear_dims",
+    "gnot_plan_bind_params", "gnot_plan_set_batch", "gnot_plan_workspace_bytes",
+    "gnot_plan_bind_workspace", "gnot_plan_grad_offsets", "gnot_pack_weights", "gnot_forward",
+    "gnot_backward", "gnot_debug_buffer", "gnot_last_error", "gnot_version",
+]
+
+
+def build(jobs=8, quiet=True):
+    """Compile the HIP sources for gfx950 into lib/libgnot_hip.so (hipcc cross-compiles, no GPU)."""
+    cmd = ["make", "-C", CSRC, f"-j{jobs}"]
+    res = subprocess.run(cmd, capture_output=quiet, text=True)
+    if res.returncode != 0:
+        raise RuntimeError("building libgnot_hip.so failed:\n" + (res.stdout or "") + (res.stderr or ""))
+    return LIB_PATH
+
+
+def _declare(lib):
+    P = ctypes.c_void_p
+    i32, i64, sz = ctypes.c_int, ctypes.c_int64, ctypes.c_size_t
+    lib.gnot_plan_create.argtypes = [ctypes.POINTER(GnotConfig), ctypes.POINTER(P)]
+    lib.gnot_plan_destroy.argtypes = [P]
+    lib.gnot_plan_destroy.restype = None
+    lib.gnot_plan_num_linears.argtypes = [P]
+    lib.gnot_plan_linear_dims.argtypes = [P, ctypes.POINTER(ctypes.c_int32)]
+    lib.gnot_plan_bind_params.argtypes = [P, ctypes.POINTER(P), ctypes.POINTER(P)]
+    lib.gnot_plan_set_batch.argtypes = [P, i32, ctypes.POINTER(i64), ctypes.POINTER(i64), i32]
+    lib.gnot_plan_workspace_bytes.argtypes = [P]
+    lib.gnot_plan_workspace_bytes.restype = sz
+    lib.gnot_plan_bind_workspace.argtypes = [P, P, sz]
+    lib.gnot_plan_grad_offsets.argtypes = [P, ctypes.POINTER(i64)]
+    lib.gnot_pack_weights.argtypes = [P, P]
+    lib.gnot_forward.argtypes = [P, P, P, ctypes.POINTER(P), P, P]
+    lib.gnot_backward.argtypes = [P, P, P]
+    lib.gnot_debug_buffer.argtypes = [P, ctypes.c_char_p, ctypes.POINTER(P), ctypes.POINTER(i64)]
+    lib.gnot_last_error.restype = ctypes.c_char_p
+    lib.gnot_last_error.argtypes = []
+    lib.gnot_version.restype = ctypes.c_char_p
+    lib.gnot_version.argtypes = []
+    return lib
+
+
+_LIB = None
+
+
+def load():
+    """Load libgnot_hip.so (raises if it is missing: there is no CPU fallback)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not found: build it with `make -C {CSRC}` "
+                              "(gnot_amd has no CPU fallback)")
+        _LIB = _declare(ctypes.CDLL(LIB_PATH))
+    return _LIB
+
+
+def check(rc):
+    if rc != 0:
+        raise RuntimeError(f"libgnot_hip error {rc}: {load().gnot_last_error().decode()}")

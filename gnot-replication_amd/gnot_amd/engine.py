@@ -1,0 +1,122 @@
+"""Host-side owner of one `gnot_plan`: parameters, batch geometry, workspace, grads.
+
+All device memory is a torch tensor (the PyTorch caching allocator owns it); the native library
+only receives pointers.  Kernel launches go on torch's current HIP stream.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+
+
+def _ptr_array(ptrs):
+    return (ctypes.c_void_p * len(ptrs))(*ptrs)
+
+
+class Engine:
+    def __init__(self, cfg: dict, linears):
+        """cfg: the 12 constructor arguments; linears: nn.Linear modules in state_dict order."""
+        self.lib = _lib.load()
+        c = _lib.GnotConfig(**cfg)
+        plan = ctypes.c_void_p()
+        _lib.check(self.lib.gnot_plan_create(ctypes.byref(c), ctypes.byref(plan)))
+        self.plan = plan
+        n = self.lib.gnot_plan_num_linears(plan)
+        dims = (ctypes.c_int32 * (2 * n))()
+        _lib.check(self.lib.gnot_plan_linear_dims(plan, dims))
+        self.dims = [(dims[2 * i], dims[2 * i + 1]) for i in range(n)]
+        if len(linears) != n:
+            raise RuntimeError(f"expected {n} Linears, module has {len(linears)}")
+        for (o, i), lin in zip(self.dims, linears):
+            if tuple(lin.weight.shape) != (o, i):
+                raise RuntimeError(f"Linear shape {tuple(lin.weight.shape)} != plan {(o, i)}")
+        self.linears = list(linears)
+        self._bound_ptrs = None
+        self.geom = None
+        self.ws = None
+        self.grad_views = None
+        self.fwd_token = 0
+
+    def __del__(self):
+        try:
+            if getattr(self, "plan", None):
+                self.lib.gnot_plan_destroy(self.plan)
+        except Exception:
+            pass
+
+    # ---------------------------------------------------------------- binding
+    def _bind_params(self):
+        ws = [lin.weight for lin in self.linears]
+        bs = [lin.bias for lin in self.linears]
+        for t in ws + bs:
+            if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()):
+                raise RuntimeError("gnot_amd parameters must be contiguous float32 on a ROCm GPU")
+        ptrs = tuple(t.data_ptr() for t in ws + bs)
+        if ptrs != self._bound_ptrs:
+            n = len(ws)
+            _lib.check(self.lib.gnot_plan_bind_params(self.plan, _ptr_array(ptrs[:n]), _ptr_array(ptrs[n:])))
+            self._bound_ptrs = ptrs
+            self.geom = None   # workspace tables embed parameter pointers: rebind
+
+    def prepare(self, x_off, fn_offs, training, device):
+        """Set batch geometry (host int lists) and (re)bind the workspace when it changed."""
+        self._bind_params()
+        geom = (tuple(x_off), tuple(tuple(o) for o in fn_offs), bool(training))
+        if geom == self.geom:
+            return
+        B = len(x_off) - 1
+        xo = (ctypes.c_int64 * (B + 1))(*x_off)
+        flat = [v for o in fn_offs for v in o]
+        fo = (ctypes.c_int64 * max(1, len(flat)))(*flat) if flat else None
+        _lib.check(self.lib.gnot_plan_set_batch(self.plan, B, xo, fo, int(training)))
+        need = self.lib.gnot_plan_workspace_bytes(self.plan)
+        if self.ws is None or self.ws.numel() < need or self.ws.device != device:
+            self.ws = None
+            self.ws = torch.empty(need + 256, dtype=torch.uint8, device=device)
+        torch.cuda.current_stream(device).synchronize()
+        _lib.check(self.lib.gnot_plan_bind_workspace(self.plan, self.ws.data_ptr(), self.ws.numel()))
+        self.geom = geom
+        self.grad_views = None
+        if training:
+            n = len(self.dims)
+            offs = (ctypes.c_int64 * (2 * n))()
+            _lib.check(self.lib.gnot_plan_grad_offsets(self.plan, offs))
+            base = self.debug_ptr("grads")[0] - self.ws.data_ptr()
+            wsf = self.ws[: (self.ws.numel() // 4) * 4].view(torch.float32)
+            views = []
+            for k, (o, i) in enumerate(self.dims):
+                wo = base // 4 + offs[2 * k]
+                bo = base // 4 + offs[2 * k + 1]
+                views.append((wsf[wo:wo + o * i].view(o, i), wsf[bo:bo + o]))
+            self.grad_views = views
+
+    def debug_ptr(self, name):
+        ptr = ctypes.c_void_p()
+        ld = ctypes.c_int64()
+        _lib.check(self.lib.gnot_debug_buffer(self.plan, name.encode(), ctypes.byref(ptr), ctypes.byref(ld)))
+        return ptr.value, ld.value
+
+    def debug_tensor(self, name, rows, cols):
+        """Copy of a named workspace buffer as a [rows, cols] float32 tensor (tests / debugging)."""
+        ptr, ld = self.debug_ptr(name)
+        off = (ptr - self.ws.data_ptr()) // 4
+        wsf = self.ws[: (self.ws.numel() // 4) * 4].view(torch.float32)
+        ld = ld if ld > 0 else cols
+        return wsf[off:off + rows * ld].view(rows, ld)[:, :cols].clone()
+
+    # ---------------------------------------------------------------- compute
+    def stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def forward(self, x, theta, fns, out):
+        s = self.stream()
+        _lib.check(self.lib.gnot_pack_weights(self.plan, s))
+        fptr = _ptr_array([f.data_ptr() for f in fns]) if fns else None
+        _lib.check(self.lib.gnot_forward(self.plan, x.data_ptr(), theta.data_ptr(), fptr, out.data_ptr(), s))
+        self.fwd_token += 1
+        return self.fwd_token
+
+    def backward(self, dout):
+        _lib.check(self.lib.gnot_backward(self.plan, dout.data_ptr(), self.stream()))
+        return self.grad_views

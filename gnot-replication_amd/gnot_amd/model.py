@@ -1,0 +1,181 @@
+"""Drop-in `GNOT` module backed by the MI355X HIP kernels.
+
+Mirrors the reference interface exactly (aloe101/GNOT-Replication, model.py):
+  * same class names and constructor signatures            (model.py:5-7, 33-34, 118-119, 142-143)
+  * same submodule structure, hence identical `state_dict` keys, shapes and order, so checkpoints
+    saved by main.py:151 load unchanged
+  * same forward signature `forward(x, theta, input_functions=None)` -> [B, N, out_dim]
+    (model.py:154); input_functions may be the stacked [I, B, M, F] tensor main.py:82 builds or a
+    list of [B, M_i, F] tensors
+  * same error behaviour: `n_embed should be divisible by head` assertion (model.py:41) and a
+    NotImplementedError when input functions are required but not given (model.py:89 calls a
+    ModuleList in that case)
+
+Only the whole-model forward/backward runs on the GPU through libgnot_hip.so (one autograd
+Function); the submodules exist to own the parameters.  There is no CPU path: on a tensor that is
+not on a ROCm device the forward raises.
+"""
+import torch
+import torch.nn as nn
+
+from .engine import Engine
+
+
+class MLP(nn.Module):
+    """Parameter container with the reference's layout (model.py:5-18)."""
+
+    def __init__(self, num_layers, input_dim, hidden_dim, output_dim):
+        super().__init__()
+        layers = [nn.Linear(input_dim, hidden_dim), nn.GELU()]
+        for _ in range(num_layers - 1):
+            layers += [nn.Linear(hidden_dim, hidden_dim), nn.GELU()]
+        layers.append(nn.Linear(hidden_dim, output_dim))
+        self.layers = nn.Sequential(*layers)
+
+    def linears(self):
+        return [m for m in self.layers if isinstance(m, nn.Linear)]
+
+
+class LinearAttention(nn.Module):
+    """Parameter container of the normalized linear attention (model.py:33-51)."""
+
+    def __init__(self, n_embed, head, n_input_functions=0):
+        super().__init__()
+        self.head = head
+        self.n_embed = n_embed
+        self.n_input_functions = n_input_functions
+        self.head_dim = n_embed // head
+        assert self.head_dim * head == n_embed, "n_embed should be divisible by head"
+        self.query = nn.Linear(n_embed, n_embed)
+        self.fc_out = nn.Linear(n_embed, n_embed)
+        if self.n_input_functions > 0:
+            self.key = nn.ModuleList([nn.Linear(n_embed, n_embed) for _ in range(n_input_functions)])
+            self.value = nn.ModuleList([nn.Linear(n_embed, n_embed) for _ in range(n_input_functions)])
+        else:
+            self.key = nn.Linear(n_embed, n_embed)
+            self.value = nn.Linear(n_embed, n_embed)
+
+    def linears(self):
+        keys = list(self.key) if isinstance(self.key, nn.ModuleList) else [self.key]
+        values = list(self.value) if isinstance(self.value, nn.ModuleList) else [self.value]
+        return [self.query, self.fc_out] + keys + values
+
+
+class HeterogeneousNormalizedAttentionBlock(nn.Module):
+    """Parameter container of one GNOT block (model.py:118-124)."""
+
+    def __init__(self, n_attn_hidden_dim, n_mlp_num_layers, n_mlp_hidden_dim, n_input_hidden_dim, n_expert,
+                 n_head, n_input_functions=0):
+        super().__init__()
+        self.cross_attention = LinearAttention(n_attn_hidden_dim, n_head, n_input_functions)
+        self.self_attention = LinearAttention(n_attn_hidden_dim, n_head)
+        self.ffn1 = nn.ModuleList(MLP(n_mlp_num_layers, n_input_hidden_dim, n_mlp_hidden_dim, n_mlp_hidden_dim)
+                                  for _ in range(n_expert))
+        self.ffn2 = nn.ModuleList(MLP(n_mlp_num_layers, n_input_hidden_dim, n_mlp_hidden_dim, n_mlp_hidden_dim)
+                                  for _ in range(n_expert))
+
+    def linears(self):
+        out = self.cross_attention.linears() + self.self_attention.linears()
+        for m in list(self.ffn1) + list(self.ffn2):
+            out += m.linears()
+        return out
+
+
+class _GNOTFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, engine, x, theta, fns, out_dim, *params):
+        P = x.shape[0]
+        out = torch.empty(P, out_dim, device=x.device, dtype=torch.float32)
+        ctx.engine = engine
+        ctx.token = engine.forward(x, theta, fns, out)
+        ctx.nparams = len(params)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        eng = ctx.engine
+        if eng.fwd_token != ctx.token:
+            raise RuntimeError("gnot_amd keeps the activations of the most recent forward only; "
+                               "backward must follow its own forward")
+        views = eng.backward(dout.contiguous().float())
+        grads = []
+        for w, b in views:
+            grads += [w.clone(), b.clone()]
+        # params were passed as (all weights..., all biases...)
+        n = len(views)
+        ordered = [grads[2 * k] for k in range(n)] + [grads[2 * k + 1] for k in range(n)]
+        return (None, None, None, None, None, *ordered)
+
+
+class GNOT(nn.Module):
+    """Drop-in replacement of the reference GNOT (model.py:142-173)."""
+
+    def __init__(self, input_dim, theta_dim, input_func_dim, out_dim, n_attn_layers, n_attn_hidden_dim,
+                 n_mlp_num_layers, n_mlp_hidden_dim, n_input_hidden_dim, n_expert, n_head, n_input_functions=0):
+        super().__init__()
+        self.x = MLP(n_mlp_num_layers, input_dim + theta_dim, n_input_hidden_dim, n_input_hidden_dim)
+        self.gating = MLP(n_mlp_num_layers, input_dim, n_mlp_hidden_dim, n_expert)
+        self.input_func_mlps = nn.ModuleList(MLP(n_mlp_num_layers, input_func_dim, n_mlp_hidden_dim,
+                                                 n_input_hidden_dim) for _ in range(n_input_functions))
+        self.blocks = nn.ModuleList(HeterogeneousNormalizedAttentionBlock(
+            n_attn_hidden_dim, n_mlp_num_layers, n_mlp_hidden_dim, n_input_hidden_dim, n_expert, n_head,
+            n_input_functions) for _ in range(n_attn_layers))
+        self.out = MLP(n_mlp_num_layers, n_input_hidden_dim, n_mlp_hidden_dim, out_dim)
+        self._cfg = dict(input_dim=input_dim, theta_dim=theta_dim, input_func_dim=input_func_dim,
+                         out_dim=out_dim, n_attn_layers=n_attn_layers, n_attn_hidden_dim=n_attn_hidden_dim,
+                         n_mlp_num_layers=n_mlp_num_layers, n_mlp_hidden_dim=n_mlp_hidden_dim,
+                         n_input_hidden_dim=n_input_hidden_dim, n_expert=n_expert, n_head=n_head,
+                         n_input_functions=n_input_functions)
+        self._engine = None
+
+    # canonical Linear order == named_parameters() order of the reference module
+    def linears(self):
+        out = self.x.linears() + self.gating.linears()
+        for m in self.input_func_mlps:
+            out += m.linears()
+        for blk in self.blocks:
+            out += blk.linears()
+        return out + self.out.linears()
+
+    def engine(self):
+        if self._engine is None:
+            self._engine = Engine(self._cfg, self.linears())
+        return self._engine
+
+    def _apply(self, fn, *args, **kwargs):
+        # moving / casting the module invalidates the bound parameter pointers
+        self._engine = None
+        return super()._apply(fn, *args, **kwargs)
+
+    def forward(self, x, theta, input_functions=None):
+        """Reference calling convention (model.py:154): zero-padded batch x [B, N, input_dim]."""
+        B, N, _ = x.shape
+        I = self._cfg["n_input_functions"]
+        fns, fn_offs = [], []
+        if I > 0:
+            if input_functions is None:
+                # model.py:88-89: the self branch calls the key ModuleList -> NotImplementedError
+                raise NotImplementedError("GNOT with n_input_functions > 0 needs input_functions")
+            for i in range(I):
+                f = input_functions[i]
+                M = f.shape[1]
+                fns.append(f.reshape(B * M, f.shape[-1]))
+                fn_offs.append([b * M for b in range(B + 1)])
+        x_off = [b * N for b in range(B + 1)]
+        out = self.forward_packed(x.reshape(B * N, x.shape[-1]), x_off, theta, fns, fn_offs)
+        return out.view(B, N, -1)
+
+    def forward_packed(self, x, x_off, theta, fns=(), fn_offs=()):
+        """Packed-offsets forward (no padding): x [sum N_b, input_dim] with host offsets x_off [B+1];
+        fns[i] [sum M_ib, input_func_dim] with fn_offs[i] [B+1].  Equals one B=1 reference call per
+        sample, concatenated.  Returns [sum N_b, out_dim]."""
+        if not x.is_cuda:
+            raise RuntimeError("gnot_amd runs on a ROCm GPU only (libgnot_hip.so); no CPU path")
+        x = x.contiguous().float()
+        theta = theta.contiguous().float()
+        fns = [f.contiguous().float() for f in fns]
+        params = [l.weight for l in self.linears()] + [l.bias for l in self.linears()]
+        training = torch.is_grad_enabled() and any(p.requires_grad for p in params)
+        eng = self.engine()
+        eng.prepare([int(v) for v in x_off], [[int(v) for v in o] for o in fn_offs], training, x.device)
+        return _GNOTFunction.apply(eng, x, theta, fns, self._cfg["out_dim"], *params)

@@ -1,0 +1,111 @@
+/* gnot_hip.h — C ABI of the MI355X-native GNOT core (libgnot_hip.so).
+ *
+ * Drop-in boundary for the reference's hot path: `GNOT.forward` (reference model.py:154-173) and the
+ * backward that `loss.backward()` (main.py:102) runs through it.  The reference is pure PyTorch and
+ * has no FFI; these entry points are what its `GNOT` module binds in our host mirror
+ * (gnot-replication_amd/gnot_amd/model.py, via ctypes — see INTEGRATION.md):
+ *
+ *   reference                                   replaced by
+ *   GNOT.__init__(...)            model.py:143   gnot_plan_create (same 12 constructor arguments)
+ *   nn.Linear parameters          model.py:9-14, 43-51  gnot_plan_bind_params (state_dict order)
+ *   padding / batching       utils.py:3-4, main.py:60-89  gnot_plan_set_batch (packed offsets)
+ *   GNOT.forward                  model.py:154-173  gnot_forward
+ *   autograd backward             main.py:102    gnot_backward
+ *
+ * Conventions: plain pointers and sizes only, no torch types.  All device memory (inputs, outputs,
+ * parameters, the workspace) is allocated and owned by the caller; the library never allocates
+ * device memory.  Every compute entry point is asynchronous and stream-ordered on the hipStream_t
+ * it is given (pass NULL for the default stream), launches kernels only (graph-capturable) and
+ * returns 0 on success or a negative GNOT_E* code; gnot_last_error() then describes the failure.
+ */
+#ifndef GNOT_HIP_H
+#define GNOT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct gnot_plan gnot_plan; /* opaque */
+
+/* GNOT constructor arguments, reference model.py:143 (positional order of main.py:44).
+ * n_attn_hidden_dim, n_mlp_hidden_dim and n_input_hidden_dim must be equal (the reference's
+ * residual adds, model.py:131/137, require it); d % 16 == 0, d/n_head in {4, 8, 16, 32, 48, 64}. */
+typedef struct gnot_config {
+  int input_dim;
+  int theta_dim;
+  int input_func_dim;
+  int out_dim;
+  int n_attn_layers;
+  int n_attn_hidden_dim;
+  int n_mlp_num_layers;
+  int n_mlp_hidden_dim;
+  int n_input_hidden_dim;
+  int n_expert;
+  int n_head;
+  int n_input_functions;
+} gnot_config;
+
+enum {
+  GNOT_OK = 0,
+  GNOT_E_INVALID = -1,     /* bad argument / unsupported configuration */
+  GNOT_E_HIP = -2,         /* a HIP runtime call failed */
+  GNOT_E_STATE = -3,       /* call out of order (e.g. forward before bind) */
+  GNOT_E_WORKSPACE = -4    /* workspace missing or too small */
+};
+
+/* Plan lifetime. */
+int gnot_plan_create(const gnot_config* cfg, gnot_plan** out);
+void gnot_plan_destroy(gnot_plan* plan);
+
+/* Linears in reference state_dict order (named_parameters() order of model.py's GNOT).
+ * dims[2*i] = out_features, dims[2*i+1] = in_features. */
+int gnot_plan_num_linears(const gnot_plan* plan);
+int gnot_plan_linear_dims(const gnot_plan* plan, int32_t* dims);
+
+/* Device pointers of every Linear's weight [out, in] (row-major) and bias [out], fp32, in the order
+ * above.  Pointers must stay valid (parameters are updated in place by the optimizer). */
+int gnot_plan_bind_params(gnot_plan* plan, const float* const* weights, const float* const* biases);
+
+/* Batch geometry.  x_off: host array [B+1] of point offsets (packed, no padding: sample b owns rows
+ * x_off[b] .. x_off[b+1]-1); fn_off: host array [n_input_functions * (B+1)] of the same for every
+ * input function.  A zero-padded batch (main.py:60-82) is simply x_off = {0, N, 2N, ...}.
+ * training != 0 keeps the activations the backward needs. */
+int gnot_plan_set_batch(gnot_plan* plan, int B, const int64_t* x_off, const int64_t* fn_off, int training);
+
+/* Workspace: bytes needed for the current config + batch; bind a device buffer of at least that
+ * size (256-byte aligned).  Binding uploads the plan's small device tables (synchronous). */
+size_t gnot_plan_workspace_bytes(const gnot_plan* plan);
+int gnot_plan_bind_workspace(gnot_plan* plan, void* workspace, size_t bytes);
+
+/* Parameter-gradient arena inside the workspace: offsets (in floats) of every Linear's weight
+ * gradient and bias gradient, grad_off[2*i] / grad_off[2*i+1]. */
+int gnot_plan_grad_offsets(const gnot_plan* plan, int64_t* grad_off);
+
+/* Re-pack the bound parameters into the kernels' MFMA operand images (call after every optimizer
+ * step, before gnot_forward). */
+int gnot_pack_weights(gnot_plan* plan, void* stream);
+
+/* Forward (reference GNOT.forward, model.py:154-173).
+ * x [P, input_dim], theta [B, theta_dim], fns[i] [Q_i, input_func_dim] (packed, device, fp32,
+ * contiguous); out [P, out_dim]. */
+int gnot_forward(gnot_plan* plan, const float* x, const float* theta, const float* const* fns,
+                 float* out, void* stream);
+
+/* Backward of the last gnot_forward: dout [P, out_dim] -> every parameter gradient, written
+ * (overwritten) into the gradient arena. */
+int gnot_backward(gnot_plan* plan, const float* dout, void* stream);
+
+/* Debug/test hook: device pointer + row stride (floats) of a named intermediate buffer
+ * ("scores", "query0", "out_h0", ...); returns GNOT_E_INVALID for unknown names. */
+int gnot_debug_buffer(const gnot_plan* plan, const char* name, float** ptr, int64_t* ld);
+
+const char* gnot_last_error(void);
+const char* gnot_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GNOT_HIP_H */

@@ -1,0 +1,124 @@
+"""CPU-side checks of the drop-in boundary: state_dict layout, the C ABI library, plan logic."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from golden_util import fixture_names, load, model_args
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "gnot_hip.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|size_t|const char\*)\s+(gnot_\w+)\s*\(", src, re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    from gnot_amd import _lib
+    lib = _lib.load()
+    names = header_functions()
+    assert len(names) >= 15
+    for n in names:
+        assert hasattr(lib, n), n
+    assert sorted(_lib.EXPORTS) == names
+    assert b"gfx950" in lib.gnot_version()
+
+
+@pytest.mark.parametrize("name", fixture_names())
+def test_state_dict_matches_reference(name):
+    """Same keys, order and shapes as the reference module -> checkpoints interchange."""
+    from gnot_amd import GNOT
+    fx = load(name)
+    m = GNOT(*model_args(fx["cfg"]))
+    sd = m.state_dict()
+    assert list(sd.keys()) == list(fx["params"].keys())
+    for k, v in sd.items():
+        assert tuple(v.shape) == fx["params"][k].shape, k
+    m.load_state_dict({k: torch.from_numpy(v).float() for k, v in fx["params"].items()})
+
+
+@pytest.mark.parametrize("name", fixture_names())
+def test_plan_linear_order_matches_module(name):
+    """The native plan's canonical Linear list == the module's named_parameters order."""
+    from gnot_amd import GNOT
+    from gnot_amd import _lib
+    fx = load(name)
+    m = GNOT(*model_args(fx["cfg"]))
+    lin = m.linears()
+    names = [k[:-len(".weight")] for k in m.state_dict() if k.endswith(".weight")]
+    assert len(names) == len(lin)
+    lib = _lib.load()
+    cfg = _lib.GnotConfig(**m._cfg)
+    plan = ctypes.c_void_p()
+    _lib.check(lib.gnot_plan_create(ctypes.byref(cfg), ctypes.byref(plan)))
+    try:
+        n = lib.gnot_plan_num_linears(plan)
+        dims = (ctypes.c_int32 * (2 * n))()
+        _lib.check(lib.gnot_plan_linear_dims(plan, dims))
+        assert n == len(lin)
+        for k, l in enumerate(lin):
+            assert (dims[2 * k], dims[2 * k + 1]) == tuple(l.weight.shape)
+        # batch geometry + workspace sizing are host-only
+        B = len(fx["x_off"]) - 1
+        xo = (ctypes.c_int64 * (B + 1))(*[int(v) for v in fx["x_off"]])
+        flat = [int(v) for o in fx["fn_offs"] for v in o]
+        fo = (ctypes.c_int64 * max(1, len(flat)))(*flat)
+        _lib.check(lib.gnot_plan_set_batch(plan, B, xo, fo if flat else None, 1))
+        need = lib.gnot_plan_workspace_bytes(plan)
+        assert need > 0
+        offs = (ctypes.c_int64 * (2 * n))()
+        _lib.check(lib.gnot_plan_grad_offsets(plan, offs))
+        total = sum(o * i + o for o, i in (tuple(l.weight.shape) for l in lin))
+        assert offs[2 * n - 1] + lin[-1].weight.shape[0] == total
+    finally:
+        lib.gnot_plan_destroy(plan)
+
+
+def test_constructor_errors_mirror_reference():
+    from gnot_amd import GNOT
+    with pytest.raises(AssertionError, match="divisible by head"):
+        GNOT(2, 1, 3, 1, 1, 32, 2, 32, 32, 2, 5, 1)
+
+
+def test_plan_rejects_bad_config_and_batch():
+    from gnot_amd import _lib
+    lib = _lib.load()
+    good = dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=1, n_attn_hidden_dim=32,
+                n_mlp_num_layers=2, n_mlp_hidden_dim=32, n_input_hidden_dim=32, n_expert=2, n_head=4,
+                n_input_functions=1)
+    plan = ctypes.c_void_p()
+    for bad in (dict(n_mlp_hidden_dim=64), dict(n_head=5), dict(n_attn_hidden_dim=40, n_mlp_hidden_dim=40,
+                                                                  n_input_hidden_dim=40)):
+        cfg = _lib.GnotConfig(**{**good, **bad})
+        assert lib.gnot_plan_create(ctypes.byref(cfg), ctypes.byref(plan)) == -1
+        assert lib.gnot_last_error()
+    cfg = _lib.GnotConfig(**good)
+    _lib.check(lib.gnot_plan_create(ctypes.byref(cfg), ctypes.byref(plan)))
+    try:
+        xo = (ctypes.c_int64 * 3)(0, 5, 3)         # decreasing
+        fo = (ctypes.c_int64 * 3)(0, 2, 4)
+        assert lib.gnot_plan_set_batch(plan, 2, xo, fo, 1) == -1
+        xo = (ctypes.c_int64 * 3)(0, 5, 9)
+        assert lib.gnot_plan_set_batch(plan, 2, xo, None, 1) == -1   # fn offsets required
+        assert lib.gnot_forward(plan, None, None, None, None, None) == -3   # not bound
+    finally:
+        lib.gnot_plan_destroy(plan)
+
+
+def test_forward_refuses_cpu_tensors():
+    from gnot_amd import GNOT
+    m = GNOT(2, 1, 3, 1, 1, 32, 2, 32, 32, 2, 4, 0)
+    with pytest.raises(RuntimeError, match="ROCm GPU"):
+        m(torch.rand(1, 10, 2), torch.rand(1, 1))
+
+
+def test_missing_input_functions_raises_like_reference():
+    from gnot_amd import GNOT
+    m = GNOT(2, 1, 3, 1, 1, 32, 2, 32, 32, 2, 4, 1)
+    with pytest.raises(NotImplementedError):
+        m(torch.rand(1, 10, 2), torch.rand(1, 1))
