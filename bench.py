@@ -1,0 +1,236 @@
+#!/usr/bin/env python3
+"""GNOT fwd+bwd training-step benchmark on MI355X (the driver's bench contract).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload = BASELINE.json configs[1] (the metric's single-GPU configuration): GNOT with 4 blocks,
+4 experts, hidden 128, 8 heads, 4-layer MLPs, 2 input functions (multi-input cross-attention),
+one 2-D irregular mesh of 10,000 query points per GPU with 805 points per input function, fp32
+(the reference computes in fp32).  A step = pack weights -> GNOT forward (gnot_amd, HIP) -> RelL2
+loss (loss.py:14-23, per-sample segment sums) -> backward to every parameter gradient ->
+(N>1: one RCCL all-reduce of the flat gradient arena, sample-data-parallel) -> AdamW step.
+Multi-GPU scaling is weak: every rank owns its own mesh (SURVEY.md §8e sample-DP).
+
+value = all query points processed by all ranks / max-over-ranks wall time of the K timed steps.
+roofline: the dominant kernel (fused MoE expert chains, backward) timed live with hipEvents on
+its own stream during the timed steps; achieved = its algorithmic MFMA FLOPs / device time vs the
+fp32 MFMA peak (157.3 TFLOP/s, MI355X_MICROARCH.md).
+cpu_baseline: the stock-torch CPU port of the reference (oracle/torch_port.py) on this host's
+cores, same workload, rank 0 at N=1 only.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gnot-replication_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 / 32x32x2, dense
+HBM_PEAK_GBS = 8000.0
+
+WORKLOADS = {
+    # BASELINE.json configs[1]
+    "cfg2": dict(model=dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=4,
+                            n_attn_hidden_dim=128, n_mlp_num_layers=4, n_mlp_hidden_dim=128,
+                            n_input_hidden_dim=128, n_expert=4, n_head=8, n_input_functions=2),
+                 N=10000, M=805, B=1,
+                 desc="configs[1]: GNOT 4-layer, 4-expert, d=128, 8 heads, 2 input functions, "
+                      "2-D irregular mesh 10k points/sample (805 points per input function), fp32 fwd+bwd"),
+    # BASELINE.json configs[0] (main.py defaults, ~1-4k points/sample, batch 4)
+    "cfg1": dict(model=dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=4,
+                            n_attn_hidden_dim=256, n_mlp_num_layers=4, n_mlp_hidden_dim=256,
+                            n_input_hidden_dim=256, n_expert=3, n_head=8, n_input_functions=1),
+                 N=4096, M=805, B=4,
+                 desc="configs[0]: main.py defaults d=256, 3 experts, 8 heads, 1 input function, "
+                      "batch 4 x 4096 points, fp32 fwd+bwd"),
+}
+
+
+def rel_l2_loss(out, tgt, seg, B):
+    """RelL2Loss (loss.py:14-23): mean over samples x channels of sqrt(sum (p-t)^2 / sum t^2)."""
+    C = out.shape[1]
+    num = torch.zeros(B, C, device=out.device).index_add_(0, seg, (out - tgt) ** 2)
+    den = torch.zeros(B, C, device=out.device).index_add_(0, seg, tgt ** 2)
+    return (num / den).sqrt().mean()
+
+
+def make_batch(w, seed, device):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    m = w["model"]
+    B, N, M = w["B"], w["N"], w["M"]
+    x = torch.rand(B * N, m["input_dim"], generator=g)
+    theta = torch.rand(B, m["theta_dim"], generator=g)
+    fns = [torch.rand(B * M, m["input_func_dim"], generator=g) for _ in range(m["n_input_functions"])]
+    y = torch.randn(B * N, m["out_dim"], generator=g)
+    x_off = [b * N for b in range(B + 1)]
+    fn_offs = [[b * M for b in range(B + 1)] for _ in range(m["n_input_functions"])]
+    seg = torch.repeat_interleave(torch.arange(B), N)
+    to = lambda t: t.to(device)
+    return to(x), x_off, to(theta), [to(f) for f in fns], fn_offs, to(y), to(seg)
+
+
+def cpu_baseline(w, steps=5, warmup=2):
+    """Reference CPU path (stock torch, oracle/torch_port.py) on this host's cores."""
+    from oracle import torch_port
+    from gnot_amd import GNOT
+    m = w["model"]
+    torch.manual_seed(0)
+    mod = GNOT(*[m[k] for k in ("input_dim", "theta_dim", "input_func_dim", "out_dim", "n_attn_layers",
+                                "n_attn_hidden_dim", "n_mlp_num_layers", "n_mlp_hidden_dim",
+                                "n_input_hidden_dim", "n_expert", "n_head", "n_input_functions")])
+    p = {k: v.detach().clone().requires_grad_(True) for k, v in mod.state_dict().items()}
+    cfg = dict(m, d=m["n_attn_hidden_dim"])
+    x, x_off, theta, fns, fn_offs, y, seg = make_batch(w, 0, torch.device("cpu"))
+    B, N, M = w["B"], w["N"], w["M"]
+    xb = x.view(B, N, -1)
+    fb = [f.view(B, M, -1) for f in fns]
+    times = []
+    for it in range(warmup + steps):
+        t0 = time.perf_counter()
+        out = torch_port.gnot_forward(p, cfg, xb, theta, fb).reshape(B * N, -1)
+        loss = rel_l2_loss(out, y, seg, B)
+        for v in p.values():
+            v.grad = None
+        loss.backward()
+        if it >= warmup:
+            times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    return dict(value=round(B * N / med, 1), unit="points/s", cores=torch.get_num_threads(), kind="port",
+                sample=f"same workload ({B}x{N} points), stock-torch fp32 CPU port of the reference "
+                       f"(oracle/torch_port.py, fixture-validated), fwd+RelL2+bwd, median of {steps} "
+                       f"steps after {warmup} warm-up, {torch.get_num_threads()} threads")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
+    ap.add_argument("--points", type=int, default=0, help="override points per sample")
+    ap.add_argument("--roofline-kernel", default="moe_bwd", choices=["moe_fwd", "moe_bwd", "wgrad"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--breakdown", action="store_true", help="print per-kernel-class device time to stderr")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    w = dict(WORKLOADS[args.workload])
+    if args.points:
+        w["N"] = args.points
+    from gnot_amd import GNOT
+    m = w["model"]
+    torch.manual_seed(1234)                       # same initial weights on every rank
+    model = GNOT(*[m[k] for k in ("input_dim", "theta_dim", "input_func_dim", "out_dim", "n_attn_layers",
+                                  "n_attn_hidden_dim", "n_mlp_num_layers", "n_mlp_hidden_dim",
+                                  "n_input_hidden_dim", "n_expert", "n_head", "n_input_functions")]).to(device)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-3)          # main.py:50-51
+    x, x_off, theta, fns, fn_offs, y, seg = make_batch(w, 100 + rank, device)
+    B = w["B"]
+    eng = model.engine()
+    if world > 1:
+        eng.grad_hook = lambda g: dist.all_reduce(g, op=dist.ReduceOp.AVG)
+
+    def step():
+        out = model.forward_packed(x, x_off, theta, fns, fn_offs)
+        loss = rel_l2_loss(out, y, seg, B)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if args.breakdown:
+        for kind in ("moe_fwd", "moe_bwd", "wgrad"):
+            eng.profile_enable(kind)
+            step()
+            ms, n, fl = eng.profile_read()
+            print(f"[breakdown] {kind}: {ms:.3f} ms/step over {n} launches, "
+                  f"{fl / ms / 1e9 if ms else 0:.1f} TFLOP/s", file=sys.stderr)
+        eng.profile_enable("")
+        torch.cuda.synchronize()
+    eng.profile_enable(args.roofline_kernel)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kms, klaunch, kflops = eng.profile_read()
+    eng.profile_enable("")
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    pts = B * w["N"] * args.steps * world
+    avg_launch_ms = kms / max(klaunch, 1)
+    achieved = (kflops / max(klaunch, 1)) / (avg_launch_ms * 1e-3) / 1e12 if klaunch else 0.0
+    result = {
+        "metric": "mesh points/sec (GNOT fwd+bwd, whole node)",
+        "value": round(pts / elapsed, 1),
+        "unit": "points/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic: coords/theta/input-function rows U[0,1], targets N(0,1), seeded per rank; "
+                "random-init weights (torch.manual_seed)",
+        "config": {"workload": w["desc"], "points_per_gpu": B * w["N"], "samples_per_gpu": B,
+                   "input_function_points": w["M"], "hidden": m["n_attn_hidden_dim"], "experts": m["n_expert"],
+                   "heads": m["n_head"], "blocks": m["n_attn_layers"], "mlp_layers": m["n_mlp_num_layers"],
+                   "input_functions": m["n_input_functions"],
+                   "parallelism": f"sample-dp{world}" if world > 1 else "single",
+                   "step": "pack+fwd+RelL2+bwd+AdamW"},
+        "roofline": {
+            "kernel": {"moe_fwd": "chain_fwd_kernel (fused MoE expert chains, forward)",
+                       "moe_bwd": "chain_bwd_kernel (fused MoE expert chains, backward)",
+                       "wgrad": "wgrad_kernel+wgrad_reduce_kernel (weight gradients)"}[args.roofline_kernel],
+            "bound": "mfma",
+            "achieved": round(achieved, 3),
+            "peak": FP32_MFMA_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+            "traffic": None,
+            "avg_launch_us": round(avg_launch_ms * 1e3, 2),
+            "flops_per_launch": kflops / max(klaunch, 1),
+            "launches": klaunch,
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(w)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

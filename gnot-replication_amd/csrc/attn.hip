@@ -9,126 +9,15 @@
 // un-permuting, so the apply pass WRITES head-major per sample: element (h, n, j) of sample b lands
 // at flat offset off_b*d + (h*N_b + n)*dh + j, and fc_out reads that buffer as plain rows.
 //
-// Kernels:
-//   attn_state   per point segment: partial S and z for every head (register-blocked 4x4 outer
-//                products from an LDS-staged point tile) -> slab; attn_state_reduce sums the slabs
-//                of each sample in a fixed order (deterministic; the only cross-point reduction).
-//   attn_apply_fwd / attn_apply_bwd  one thread per (point, head).
+// Kernels here:
+//   attn_apply_fwd / attn_apply_bwd  one thread per (point, head), per-sample (S, z) staged in LDS.
 //   attn_kv_bwd  dK, dV from (dS, dz) per (source point, head).
-// The same state kernel also produces dS = sum_n q_n du_n^T and dz = sum_n dden_n q_n in the backward.
+// The cross-point reductions themselves (S, z forward; dS, dz backward) are point-reduction GEMMs
+// on the MFMA path (wgrad.hip, state jobs), one job per sample.
 #include "gnot_common.h"
 #include "gnot_kernels.h"
 
 namespace gnot {
-
-constexpr int kStateSub = 16;   // points per LDS sub-tile of the state kernel
-constexpr int kStateMaxB = 4;   // 4x4 blocks per thread -> d*dh <= 16384
-
-// segment list: chunks[c] = (b, start, len, -)
-__global__ void __launch_bounds__(256) attn_state_kernel(AttnStateArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int d = a.H * a.dh;
-  const int dhp = a.dh;
-  float* As = smem;                     // [kStateSub][d]
-  float* Bs = smem + kStateSub * d;     // [kStateSub][d]
-  float* Ws = Bs + kStateSub * d;       // [kStateSub][H]
-  const int4 ch = a.chunks[blockIdx.x];
-  const long start = ch.y;
-  const int len = ch.z;
-  const int t = threadIdx.x;
-  const int nbh = (dhp / 4) * (dhp / 4);     // 4x4 blocks per head
-  const int nblocks = a.H * nbh;
-
-  float acc[kStateMaxB][16];
-#pragma unroll
-  for (int k = 0; k < kStateMaxB; ++k)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[k][r] = 0.f;
-  float zacc = 0.f;
-
-  for (int s0 = 0; s0 < len; s0 += kStateSub) {
-    const int sl = min(kStateSub, len - s0);
-    __syncthreads();
-    for (int i = t; i < kStateSub * d; i += 256) {
-      const int n = i / d, c = i % d;
-      const bool ok = n < sl;
-      As[i] = ok ? a.A[(start + s0 + n) * a.lda + c] : 0.f;
-      Bs[i] = ok ? a.Bv[(start + s0 + n) * a.ldb + c] : 0.f;
-    }
-    for (int i = t; i < kStateSub * a.H; i += 256) {
-      const int n = i / a.H, hh = i % a.H;
-      Ws[i] = (n < sl) ? (a.w ? a.w[(start + s0 + n) * a.ldw + hh] : 1.f) : 0.f;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kStateMaxB; ++k) {
-      const int bid = t + k * 256;
-      if (bid < nblocks) {
-        const int h = bid / nbh, rem = bid % nbh;
-        const int ib = rem / (dhp / 4), jb = rem % (dhp / 4);
-        const float* ap = As + h * dhp + 4 * ib;
-        const float* bp = Bs + h * dhp + 4 * jb;
-        for (int n = 0; n < sl; ++n) {
-          const float4 av = *reinterpret_cast<const float4*>(ap + n * d);
-          const float4 bv = *reinterpret_cast<const float4*>(bp + n * d);
-          const float aa[4] = {av.x, av.y, av.z, av.w};
-          const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[k][i * 4 + j] = fmaf(aa[i], bb[j], acc[k][i * 4 + j]);
-        }
-      }
-    }
-    if (t < d) {
-      const int h = t / dhp;
-      for (int n = 0; n < sl; ++n) zacc = fmaf(Ws[n * a.H + h], As[n * d + t], zacc);
-    }
-  }
-  // slab layout per chunk: [H][dh*dh + dh]
-  const int per_head = dhp * dhp + dhp;
-  float* S = a.slab + (long)blockIdx.x * a.H * per_head;
-#pragma unroll
-  for (int k = 0; k < kStateMaxB; ++k) {
-    const int bid = t + k * 256;
-    if (bid < nblocks) {
-      const int h = bid / nbh, rem = bid % nbh;
-      const int ib = rem / (dhp / 4), jb = rem % (dhp / 4);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          S[h * per_head + (4 * ib + i) * dhp + 4 * jb + j] = acc[k][i * 4 + j];
-    }
-  }
-  if (t < d) {
-    const int h = t / dhp, i = t % dhp;
-    S[h * per_head + dhp * dhp + i] = zacc;
-  }
-}
-
-__global__ void __launch_bounds__(256) attn_state_reduce_kernel(AttnStateArgs a) {
-  const int per = a.H * (a.dh * a.dh + a.dh);
-  const int b = blockIdx.y;
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= per) return;
-  const int c0 = a.sample_chunk_off[b], c1 = a.sample_chunk_off[b + 1];
-  float s = 0.f;
-  for (int c = c0; c < c1; ++c) s += a.slab[(long)c * per + e];
-  a.state[(long)b * per + e] = s;
-}
-
-hipError_t launch_attn_state(const AttnStateArgs& a, hipStream_t s) {
-  const int d = a.H * a.dh;
-  if (a.dh % 4 != 0 || d * a.dh > 16 * 256 * kStateMaxB || d > 256 * 4) return hipErrorInvalidValue;
-  const size_t lds = (size_t)(2 * kStateSub * d + kStateSub * a.H) * sizeof(float);
-  if (a.nchunks > 0)
-    hipLaunchKernelGGL(attn_state_kernel, dim3(a.nchunks), dim3(256), lds, s, a);
-  const int per = a.H * (a.dh * a.dh + a.dh);
-  if (a.B > 0)
-    hipLaunchKernelGGL(attn_state_reduce_kernel, dim3((per + 255) / 256, a.B), dim3(256), 0, s, a);
-  return hipGetLastError();
-}
 
 // ---------------------------------------------------------------- apply (forward)
 template <int DH>

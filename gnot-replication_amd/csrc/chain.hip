@@ -17,6 +17,10 @@
 
 namespace gnot {
 
+// LDS capacity (float4) for the largest layer chunk of a width-D chain
+template <int D>
+constexpr int kLdsF4 = (D / 16) * lds_och(D / 16, D / 16) * WAVE;
+
 template <int D, int KT0, int OTL>
 __global__ void __launch_bounds__(256) chain_fwd_kernel(ChainArgs a) {
   constexpr int DT = D / 16;
@@ -27,6 +31,7 @@ __global__ void __launch_bounds__(256) chain_fwd_kernel(ChainArgs a) {
   const int e = blockIdx.y;
   const ChainLayer* L = a.layers + e * a.nlin;
   float* save = a.save ? a.save + e * a.save_chain_stride : nullptr;
+  __shared__ __attribute__((aligned(16))) float4 wlds[kLdsF4<D>];
 
   float h[DT][4];
   {
@@ -34,7 +39,7 @@ __global__ void __launch_bounds__(256) chain_fwd_kernel(ChainArgs a) {
     load_rows<KT0>(x0, a.X, a.ldx, p, valid, a.in_dim, lane);
     f32x4 acc[DT];
     init_bias<DT>(acc, L[0].bias, lane);
-    mm_tiles<KT0, DT>(L[0].Wp, x0, acc, lane);
+    mm_tiles_lds<KT0, DT>(L[0].Wp, wlds, x0, acc, 4, wave, lane);
     acc_to_regs<DT>(acc, h);
   }
   if (save) store_rows<DT>(h, save, D, p, valid, D, lane);
@@ -46,7 +51,7 @@ __global__ void __launch_bounds__(256) chain_fwd_kernel(ChainArgs a) {
   for (int l = 1; l < a.nlin - 1; ++l) {
     f32x4 acc[DT];
     init_bias<DT>(acc, L[l].bias, lane);
-    mm_tiles<DT, DT>(L[l].Wp, h, acc, lane);
+    mm_tiles_lds<DT, DT>(L[l].Wp, wlds, h, acc, 4, wave, lane);
     acc_to_regs<DT>(acc, h);
     if (save) store_rows<DT>(h, save + l * a.save_layer_stride, D, p, valid, D, lane);
 #pragma unroll
@@ -59,7 +64,7 @@ __global__ void __launch_bounds__(256) chain_fwd_kernel(ChainArgs a) {
   {
     f32x4 acc[OTL];
     init_bias<OTL>(acc, L[a.nlin - 1].bias, lane);
-    mm_tiles<DT, OTL>(L[a.nlin - 1].Wp, h, acc, lane);
+    mm_tiles_lds<DT, OTL>(L[a.nlin - 1].Wp, wlds, h, acc, 4, wave, lane);
     acc_to_regs<OTL>(acc, y);
   }
   if (save) store_rows<OTL>(y, save + (a.nlin - 1) * a.save_layer_stride, D, p, valid, 16 * OTL, lane);
@@ -115,6 +120,7 @@ __global__ void __launch_bounds__(256) chain_bwd_kernel(ChainArgs a) {
   const int e = blockIdx.y;
   const ChainLayer* L = a.layers + e * a.nlin;
   const float* save = a.save + e * a.save_chain_stride;
+  __shared__ __attribute__((aligned(16))) float4 wlds[kLdsF4<D>];
   float* dz = a.dz ? a.dz + e * a.dz_chain_stride : nullptr;
 
   // ---- gradient at the chain output
@@ -163,7 +169,7 @@ __global__ void __launch_bounds__(256) chain_bwd_kernel(ChainArgs a) {
   {
     f32x4 acc[DT];
     init_bias<DT>(acc, nullptr, lane);
-    mm_tiles<OTL, DT>(L[a.nlin - 1].WpT, dy, acc, lane);
+    mm_tiles_lds<OTL, DT>(L[a.nlin - 1].WpT, wlds, dy, acc, 4, wave, lane);
     acc_to_regs<DT>(acc, gr);
   }
   // ---- hidden Linears, reverse
@@ -177,7 +183,7 @@ __global__ void __launch_bounds__(256) chain_bwd_kernel(ChainArgs a) {
     if (dz) store_rows<DT>(gr, dz + l * a.dz_layer_stride, D, p, valid, D, lane);
     f32x4 acc[DT];
     init_bias<DT>(acc, nullptr, lane);
-    mm_tiles<DT, DT>(L[l].WpT, gr, acc, lane);
+    mm_tiles_lds<DT, DT>(L[l].WpT, wlds, gr, acc, 4, wave, lane);
     acc_to_regs<DT>(acc, gr);
   }
   // ---- first Linear
@@ -193,7 +199,7 @@ __global__ void __launch_bounds__(256) chain_bwd_kernel(ChainArgs a) {
   if (a.dX) {
     f32x4 acc[KT0];
     init_bias<KT0>(acc, nullptr, lane);
-    mm_tiles<DT, KT0>(L[0].WpT, gr, acc, lane);
+    mm_tiles_lds<DT, KT0>(L[0].WpT, wlds, gr, acc, 4, wave, lane);
     float dx[KT0][4];
     acc_to_regs<KT0>(acc, dx);
     store_rows<KT0>(dx, a.dX + e * a.dx_chain_stride, a.lddx, p, valid, a.in_dim, lane);

@@ -39,8 +39,9 @@ static inline long r4(long x) { return (x + 3) & ~3L; }
 static inline int tiles16(int x) { return (x + 15) / 16; }
 
 constexpr int kSeg = 256;            // points per attention segment (state slab / apply block)
-constexpr int kWgradChunk = 1024;    // points per split of the weight-gradient GEMM
-constexpr int kWgradMaxSplits = 64;
+constexpr int kPTile = 128;          // output tile edge of the point-reduction GEMM (wgrad.hip)
+constexpr int kTargetWGs = 512;      // aim for ~2 workgroups per CU per point-reduction launch
+constexpr int kMinSplitPoints = 128; // never split below this many points
 
 struct Img {                 // one packed MFMA A-operand image in the packed arena
   size_t off4 = 0;           // offset in float4 units
@@ -56,13 +57,12 @@ struct Buf {
 
 struct WgradGroup {
   std::vector<WgradJob> jobs;
-  int total_waves = 0, total_red = 0;
+  std::vector<int> wg_prefix, red_prefix;
+  int total_wgs = 0, total_red = 0;
   size_t slab_floats = 0;
-  // device copies
-  WgradJob* d_jobs = nullptr;
-  int* d_wave_prefix = nullptr;
+  WgradJob* d_jobs = nullptr;        // device copies (workspace tables)
+  int* d_wg_prefix = nullptr;
   int* d_red_prefix = nullptr;
-  std::vector<int> wave_prefix, red_prefix;
 };
 
 struct ChainTable {
@@ -124,8 +124,11 @@ struct gnot_plan {
   WgradGroup wg_out, wg_x, wg_gate;
   std::vector<WgradGroup> wg_fn;
   std::vector<WgradGroup> wg_m1, wg_m2, wg_self, wg_cross;
+  // attention states as point-reduction GEMM jobs (one job per sample)
+  std::vector<std::vector<WgradGroup>> st_c, dst_c;   // [l][source i]
+  std::vector<WgradGroup> st_s, dst_s;                 // [l]
   size_t table_bytes = 0;
-  size_t slab_state_floats = 0, slab_wgrad_floats = 0;
+  size_t slab_wgrad_floats = 0;
   int4* d_qchunks = nullptr;
   int* d_qchunk_off = nullptr;
   std::vector<int4*> d_fchunks;
@@ -137,6 +140,13 @@ struct gnot_plan {
   bool ws_bound = false;
   bool packed = false;
   bool fwd_done = false;
+
+  // live kernel timing (bench roofline): hipEvents around every launch of one kernel class
+  std::string prof_kind;
+  std::vector<hipEvent_t> prof_events;   // pool, pairs
+  size_t prof_used = 0;
+  double prof_flops = 0.0;
+  long prof_launches = 0;
 
   // ------------------------------------------------------------------ canonical indices
   int lin_x(int j) const { return j; }
@@ -222,7 +232,11 @@ extern "C" int gnot_plan_create(const gnot_config* cfg, gnot_plan** out) {
   return GNOT_OK;
 }
 
-extern "C" void gnot_plan_destroy(gnot_plan* plan) { delete plan; }
+extern "C" void gnot_plan_destroy(gnot_plan* plan) {
+  if (!plan) return;
+  for (hipEvent_t e : plan->prof_events) (void)hipEventDestroy(e);
+  delete plan;
+}
 
 extern "C" int gnot_plan_num_linears(const gnot_plan* p) { return p ? p->n_lin() : 0; }
 
@@ -396,6 +410,185 @@ static void plan_images(gnot_plan* p) {
   p->pack_tiles = acc;
 }
 
+// ====================================================================== point-reduction GEMM groups
+static void finish_group(gnot_plan* p, WgradGroup& G) {
+  long tiles = 0;
+  for (auto& J : G.jobs) {
+    J.tiles_o = (J.out + kPTile - 1) / kPTile;
+    J.tiles_i = (J.in + kPTile - 1) / kPTile;
+    tiles += J.diag_only ? J.tiles_o : J.tiles_o * J.tiles_i;
+  }
+  const long want = std::max<long>(1, (kTargetWGs + std::max<long>(tiles, 1) - 1) / std::max<long>(tiles, 1));
+  G.wg_prefix.clear();
+  G.red_prefix.clear();
+  G.slab_floats = 0;
+  int wg = 0, red = 0;
+  for (auto& J : G.jobs) {
+    const long maxs = std::max<long>(1, (J.P + kMinSplitPoints - 1) / kMinSplitPoints);
+    J.splits = (int)std::min<long>(std::min<long>(want, maxs), 256);
+    const int nt = J.diag_only ? J.tiles_o : J.tiles_o * J.tiles_i;
+    J.slab_off = (long)G.slab_floats;
+    G.slab_floats += (size_t)J.splits * nt * kPTile * (kPTile + 1);
+    G.wg_prefix.push_back(wg);
+    wg += nt * J.splits;
+    G.red_prefix.push_back(red);
+    red += nt * kPTile * (kPTile + 1);
+  }
+  G.total_wgs = wg;
+  G.total_red = red;
+  p->slab_wgrad_floats = std::max(p->slab_wgrad_floats, G.slab_floats);
+}
+
+template <typename F>
+static void for_each_group(gnot_plan* p, F&& f) {
+  if (p->training) {
+    f(p->wg_out); f(p->wg_x); f(p->wg_gate);
+    for (auto& G : p->wg_fn) f(G);
+    for (int l = 0; l < p->L; ++l) { f(p->wg_m1[l]); f(p->wg_m2[l]); f(p->wg_self[l]); f(p->wg_cross[l]); }
+  }
+  for (int l = 0; l < p->L; ++l) {
+    for (auto& G : p->st_c[l]) f(G);
+    f(p->st_s[l]);
+    if (p->training) {
+      for (auto& G : p->dst_c[l]) f(G);
+      f(p->dst_s[l]);
+    }
+  }
+}
+
+// (Re)build every job list from the current buffer pointers (null before bind: sizing only).
+static void build_groups(gnot_plan* p) {
+  p->slab_wgrad_floats = 0;
+  const long P = p->P;
+  const int D = p->D, NL = p->NL, E = p->E, I = p->I, KI = p->KI, dh = p->dh;
+  const bool tr = p->training;
+  const long per_state = (long)p->H * (dh * dh + dh);
+  p->wg_out = {}; p->wg_x = {}; p->wg_gate = {};
+  p->wg_fn.assign(I, {});
+  p->wg_m1.assign(p->L, {}); p->wg_m2.assign(p->L, {});
+  p->wg_self.assign(p->L, {}); p->wg_cross.assign(p->L, {});
+  p->st_c.assign(p->L, std::vector<WgradGroup>(KI));
+  p->dst_c.assign(p->L, std::vector<WgradGroup>(KI));
+  p->st_s.assign(p->L, {}); p->dst_s.assign(p->L, {});
+
+  auto lin_job = [&](WgradGroup& G, int li, const float* dz, long lddz, const float* x, long ldx, int gelu,
+                     long rows) {
+    float* grads = p->P_("grads");
+    WgradJob J{};
+    J.dz = dz; J.lddz = lddz; J.x = x; J.ldx = ldx; J.x_gelu = gelu;
+    J.out = p->lin_o[li]; J.in = p->lin_i[li];
+    J.dW = grads + p->grad_off[2 * li];
+    J.db = grads + p->grad_off[2 * li + 1];
+    J.P = (int)rows;
+    G.jobs.push_back(J);
+  };
+  // chain c of a group: Linear j reads dZ_j from dz[(c*NL + j)*rows*D] and its input from the
+  // chain input (j = 0) or gelu(saved pre-activation j-1)
+  auto chain_group = [&](WgradGroup& G, const std::vector<int>& firsts, long rows, const float* x0, long ldx0,
+                         const float* save) {
+    const float* dz = p->P_("dz");
+    for (size_t c = 0; c < firsts.size(); ++c)
+      for (int j = 0; j < NL; ++j) {
+        const float* dzp = dz + ((long)c * NL + j) * rows * D;
+        if (j == 0) lin_job(G, firsts[c] + j, dzp, D, x0, ldx0, 0, rows);
+        else lin_job(G, firsts[c] + j, dzp, D, save + ((long)c * NL + j - 1) * rows * D, D, 1, rows);
+      }
+    finish_group(p, G);
+  };
+  auto state_group = [&](WgradGroup& G, const float* A, long lda, const float* Bm, long ldb, const float* w,
+                         long ldw, const std::vector<long>& off, float* state) {
+    for (int b = 0; b < p->B; ++b) {
+      WgradJob J{};
+      J.dz = A + off[b] * lda; J.lddz = lda;
+      J.x = Bm + off[b] * ldb; J.ldx = ldb;
+      J.out = D; J.in = D;
+      J.dW = state + b * per_state;
+      J.db = J.dW;
+      J.w = w ? w + off[b] * ldw : nullptr; J.ldw = ldw; J.wdh = dh;
+      J.state_dh = dh; J.diag_only = 1;
+      J.P = (int)(off[b + 1] - off[b]);
+      G.jobs.push_back(J);
+    }
+    finish_group(p, G);
+  };
+
+  for (int l = 0; l < p->L; ++l) {
+    const std::string s = "b" + std::to_string(l) + ".";
+    // forward states
+    if (I > 0) {
+      for (int i = 0; i < I; ++i) {
+        const std::string si = std::to_string(i);
+        float* kv = p->P_(s + "ckv" + si);
+        state_group(p->st_c[l][i], kv, 2 * D, kv + D, 2 * D, nullptr, 0, p->fnoff[i], p->P_(s + "cstate" + si));
+      }
+    } else {
+      float* qkv = p->P_(s + "cq");
+      state_group(p->st_c[l][0], qkv + D, 3 * D, qkv + 2 * D, 3 * D, nullptr, 0, p->xoff, p->P_(s + "cstate0"));
+    }
+    {
+      float* qkv = p->P_(s + "sq");
+      state_group(p->st_s[l], qkv + D, 3 * D, qkv + 2 * D, 3 * D, nullptr, 0, p->xoff, p->P_(s + "sstate"));
+    }
+    if (!tr) continue;
+    // backward states dS = sum q^T du, dz = sum dden q
+    for (int i = 0; i < KI; ++i) {
+      const std::string si = std::to_string(i);
+      const long ldq = I > 0 ? D : 3 * D;
+      state_group(p->dst_c[l][i], p->P_(s + "cq"), ldq, p->P_("du" + si), D, p->P_("dden" + si), p->H, p->xoff,
+                  p->P_("dstate" + si));
+    }
+    state_group(p->dst_s[l], p->P_(s + "sq"), 3 * D, p->P_("du0"), D, p->P_("dden0"), p->H, p->xoff,
+                p->P_("dstate0"));
+  }
+  if (!tr) return;
+
+  chain_group(p->wg_out, {p->lin_out(0)}, P, p->P_(p->final_query()), D, p->P_("out_save"));
+  chain_group(p->wg_x, {p->lin_x(0)}, P, p->P_("xin"), p->bufs.at("xin").ld, p->P_("x_save"));
+  chain_group(p->wg_gate, {p->lin_g(0)}, P, p->P_("x"), p->bufs.at("x").ld, p->P_("gate_save"));
+  for (int i = 0; i < I; ++i) {
+    const std::string si = std::to_string(i);
+    chain_group(p->wg_fn[i], {p->lin_fn(i, 0)}, p->Q[i], p->P_("fn" + si), p->bufs.at("fn" + si).ld,
+                p->P_("fn_save" + si));
+  }
+  float* dsum = p->P_("dsum");
+  float* dqkv = p->P_("dqkv");
+  for (int l = 0; l < p->L; ++l) {
+    const std::string s = "b" + std::to_string(l) + ".";
+    std::vector<int> f1, f2;
+    for (int e = 0; e < E; ++e) { f1.push_back(p->lin_f1(l, e, 0)); f2.push_back(p->lin_f2(l, e, 0)); }
+    chain_group(p->wg_m1[l], f1, P, p->P_(s + "a"), D, p->P_(s + "m1save"));
+    chain_group(p->wg_m2[l], f2, P, p->P_(s + "bb"), D, p->P_(s + "m2save"));
+    {
+      WgradGroup& G = p->wg_self[l];
+      const float* q1 = p->P_(s + "query1");
+      lin_job(G, p->lin_so(l), dsum, D, p->P_(s + "sres"), D, 0, P);
+      lin_job(G, p->lin_sq(l), dqkv, 3 * D, q1, D, 0, P);
+      lin_job(G, p->lin_sk(l), dqkv + D, 3 * D, q1, D, 0, P);
+      lin_job(G, p->lin_sv(l), dqkv + 2 * D, 3 * D, q1, D, 0, P);
+      finish_group(p, G);
+    }
+    {
+      WgradGroup& G = p->wg_cross[l];
+      const float* qin = p->P_(p->block_query(l));
+      lin_job(G, p->lin_co(l), dsum, D, p->P_(s + "cres"), D, 0, P);
+      if (I > 0) {
+        lin_job(G, p->lin_cq(l), dqkv, D, qin, D, 0, P);
+        for (int i = 0; i < I; ++i) {
+          const std::string si = std::to_string(i);
+          float* dkv = p->P_("dkv" + si);
+          lin_job(G, p->lin_ck(l, i), dkv, 2 * D, p->P_("fnenc" + si), D, 0, p->Q[i]);
+          lin_job(G, p->lin_cv(l, i), dkv + D, 2 * D, p->P_("fnenc" + si), D, 0, p->Q[i]);
+        }
+      } else {
+        lin_job(G, p->lin_cq(l), dqkv, 3 * D, qin, D, 0, P);
+        lin_job(G, p->lin_ck(l, 0), dqkv + D, 3 * D, qin, D, 0, P);
+        lin_job(G, p->lin_cv(l, 0), dqkv + 2 * D, 3 * D, qin, D, 0, P);
+      }
+      finish_group(p, G);
+    }
+  }
+}
+
 extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, const int64_t* fn_off,
                                    int training) {
   if (!p || B <= 0 || !x_off) return fail(GNOT_E_INVALID, "bad batch arguments");
@@ -485,13 +678,7 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
   make_chunks(p->xoff, p->qchunks, p->qchunk_off);
   p->fchunks.assign(I, {});
   p->fchunk_off.assign(I, {});
-  size_t maxchunks = p->qchunks.size();
-  for (int i = 0; i < I; ++i) {
-    make_chunks(p->fnoff[i], p->fchunks[i], p->fchunk_off[i]);
-    maxchunks = std::max(maxchunks, p->fchunks[i].size());
-  }
-  p->slab_state_floats = maxchunks * per_state;
-  C.add("slab_state", p->slab_state_floats, 0);
+  for (int i = 0; i < I; ++i) make_chunks(p->fnoff[i], p->fchunks[i], p->fchunk_off[i]);
   if (tr) {
     C.add("dout", P * r4(p->out), r4(p->out));
     C.add("dquery", P * D, D);
@@ -525,8 +712,7 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
     T.KT0 = kt_of(in_dim);
     T.OTL = kt_of(out_dim);
     T.host.clear();
-    for (int f : firsts)
-      for (int j = 0; j < NL; ++j) T.host.push_back(ChainLayer{nullptr, nullptr, nullptr});  // filled at bind
+    T.host.assign(firsts.size() * NL, ChainLayer{nullptr, nullptr, nullptr});   // filled at bind
   };
   chain(p->ch_gate, {p->lin_g(0)}, p->in, E);
   chain(p->ch_x, {p->lin_x(0)}, p->in + p->th, (int)D);
@@ -551,78 +737,15 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
   for (int i = 0; i < I; ++i) { tbl(p->fchunks[i].size() * sizeof(int4)); tbl(p->fchunk_off[i].size() * sizeof(int)); }
   tbl((p->B + 1) * sizeof(long) * (1 + I));
 
-  // wgrad groups (pointers resolved at bind; sizes known now)
-  auto splits_of = [&](long rows) {
-    return (int)std::max<long>(1, std::min<long>(kWgradMaxSplits, (rows + kWgradChunk - 1) / kWgradChunk));
-  };
-  auto wjob = [&](WgradGroup& G, int li, long rows) {
-    WgradJob J{};
-    J.out = p->lin_o[li];
-    J.in = p->lin_i[li];
-    J.P = (int)rows;
-    J.tiles_o = (J.out + 31) / 32;
-    J.tiles_i = (J.in + 31) / 32;
-    J.splits = splits_of(rows);
-    J.slab_off = (long)G.slab_floats;
-    J.accumulate = 0;
-    // stash the linear index in dW until bind
-    J.dW = reinterpret_cast<float*>((intptr_t)li);
-    G.slab_floats += (size_t)J.splits * (J.tiles_o * 32) * (J.tiles_i * 32 + 1);
-    G.jobs.push_back(J);
-  };
-  auto finish_group = [&](WgradGroup& G) {
-    G.wave_prefix.clear();
-    G.red_prefix.clear();
-    int w = 0, r = 0;
-    for (auto& J : G.jobs) {
-      G.wave_prefix.push_back(w);
-      w += J.tiles_o * J.tiles_i * J.splits;
-      G.red_prefix.push_back(r);
-      r += (J.tiles_o * 32) * (J.tiles_i * 32 + 1);
-    }
-    G.total_waves = w;
-    G.total_red = r;
-    p->slab_wgrad_floats = std::max(p->slab_wgrad_floats, G.slab_floats);
+  // point-reduction GEMM groups: built with null buffer pointers now (sizes only), rebuilt with
+  // real pointers at bind
+  build_groups(p);
+  auto tbl_group = [&](const WgradGroup& G) {
     tbl(G.jobs.size() * sizeof(WgradJob));
     tbl(G.jobs.size() * sizeof(int) * 2);
   };
-  p->slab_wgrad_floats = 0;
-  if (tr) {
-    p->wg_out = {}; p->wg_x = {}; p->wg_gate = {};
-    for (int j = 0; j < NL; ++j) wjob(p->wg_out, p->lin_out(j), P);
-    finish_group(p->wg_out);
-    for (int j = 0; j < NL; ++j) wjob(p->wg_x, p->lin_x(j), P);
-    finish_group(p->wg_x);
-    for (int j = 0; j < NL; ++j) wjob(p->wg_gate, p->lin_g(j), P);
-    finish_group(p->wg_gate);
-    p->wg_fn.assign(I, {});
-    for (int i = 0; i < I; ++i) {
-      for (int j = 0; j < NL; ++j) wjob(p->wg_fn[i], p->lin_fn(i, j), p->Q[i]);
-      finish_group(p->wg_fn[i]);
-    }
-    p->wg_m1.assign(p->L, {}); p->wg_m2.assign(p->L, {});
-    p->wg_self.assign(p->L, {}); p->wg_cross.assign(p->L, {});
-    for (int l = 0; l < p->L; ++l) {
-      for (int e = 0; e < E; ++e)
-        for (int j = 0; j < NL; ++j) {
-          wjob(p->wg_m1[l], p->lin_f1(l, e, j), P);
-          wjob(p->wg_m2[l], p->lin_f2(l, e, j), P);
-        }
-      finish_group(p->wg_m1[l]);
-      finish_group(p->wg_m2[l]);
-      for (int li : {p->lin_so(l), p->lin_sq(l), p->lin_sk(l), p->lin_sv(l)}) wjob(p->wg_self[l], li, P);
-      finish_group(p->wg_self[l]);
-      wjob(p->wg_cross[l], p->lin_co(l), P);
-      wjob(p->wg_cross[l], p->lin_cq(l), P);
-      for (int i = 0; i < KI; ++i) {
-        const long rows = I > 0 ? p->Q[i] : P;
-        wjob(p->wg_cross[l], p->lin_ck(l, i), rows);
-        wjob(p->wg_cross[l], p->lin_cv(l, i), rows);
-      }
-      finish_group(p->wg_cross[l]);
-    }
-    C.add("slab_wgrad", p->slab_wgrad_floats, 0);
-  }
+  for_each_group(p, tbl_group);
+  C.add("slab_wgrad", p->slab_wgrad_floats, 0);
   const size_t table_off = C.raw(p->table_bytes);
   p->bufs["__tables"] = Buf{table_off, 0, nullptr};
   p->ws_need = C.top;
@@ -649,7 +772,7 @@ extern "C" int gnot_plan_bind_workspace(gnot_plan* p, void* workspace, size_t by
   if (reinterpret_cast<uintptr_t>(workspace) & 255) return fail(GNOT_E_WORKSPACE, "workspace must be 256-byte aligned");
   p->ws = static_cast<char*>(workspace);
   for (auto& kv : p->bufs) kv.second.p = reinterpret_cast<float*>(p->ws + kv.second.off);
-  const int D = p->D, NL = p->NL;
+  const int NL = p->NL;
 
   // ---- tables in the workspace tail
   char* tp = p->ws + p->bufs["__tables"].off;
@@ -719,95 +842,19 @@ extern "C" int gnot_plan_bind_workspace(gnot_plan* p, void* workspace, size_t by
     p->d_fnoff.assign(p->I, nullptr);
     for (int i = 0; i < p->I; ++i) p->d_fnoff[i] = d + (p->B + 1) * (i + 1);
   }
-  // wgrad groups
-  if (p->training) {
-    float* grads = p->P_("grads");
-    auto fill_group = [&](WgradGroup& G) {
-      std::vector<WgradJob> J = G.jobs;
-      for (auto& j : J) {
-        const int li = (int)reinterpret_cast<intptr_t>(j.dW);
-        j.dW = grads + p->grad_off[2 * li];
-        j.db = grads + p->grad_off[2 * li + 1];
-      }
-      G.jobs = J;   // dz/x pointers are set below per group
-    };
-    // dz / x sources
-    auto set_chain_src = [&](WgradGroup& G, int chain_idx, int j, const float* dz, long lddz,
-                             const float* x, long ldx, int gelu_x) {
-      WgradJob& w = G.jobs[chain_idx * NL + j];
-      w.dz = dz; w.lddz = lddz; w.x = x; w.ldx = ldx; w.x_gelu = gelu_x;
-    };
-    const long P = p->P;
-    float* dz = p->P_("dz");
-    auto chain_group = [&](WgradGroup& G, int nchains, long rows, const float* x0, long ldx0,
-                           const float* save) {
-      fill_group(G);
-      for (int e = 0; e < nchains; ++e)
-        for (int j = 0; j < NL; ++j) {
-          const float* dzp = dz + ((long)e * NL + j) * rows * D;
-          if (j == 0) set_chain_src(G, e, j, dzp, D, x0, ldx0, 0);
-          else set_chain_src(G, e, j, dzp, D, save + ((long)e * NL + (j - 1)) * rows * D, D, 1);
-        }
-    };
-    chain_group(p->wg_out, 1, P, p->P_(p->final_query()), D, p->P_("out_save"));
-    chain_group(p->wg_x, 1, P, p->P_("xin"), p->bufs["xin"].ld, p->P_("x_save"));
-    chain_group(p->wg_gate, 1, P, p->P_("x"), p->bufs["x"].ld, p->P_("gate_save"));
-    for (int i = 0; i < p->I; ++i) {
-      const std::string s = std::to_string(i);
-      chain_group(p->wg_fn[i], 1, p->Q[i], p->P_("fn" + s), p->bufs["fn" + s].ld, p->P_("fn_save" + s));
-    }
-    for (int l = 0; l < p->L; ++l) {
-      const std::string s = "b" + std::to_string(l) + ".";
-      chain_group(p->wg_m1[l], p->E, P, p->P_(s + "a"), D, p->P_(s + "m1save"));
-      chain_group(p->wg_m2[l], p->E, P, p->P_(s + "bb"), D, p->P_(s + "m2save"));
-      // self attention: Wo, Wq, Wk, Wv
-      fill_group(p->wg_self[l]);
-      {
-        auto& J = p->wg_self[l].jobs;
-        float* dqkv = p->P_("dqkv");
-        J[0].dz = p->P_("dsum"); J[0].lddz = D; J[0].x = p->P_(s + "sres"); J[0].ldx = D;
-        for (int k = 0; k < 3; ++k) {
-          J[1 + k].dz = dqkv + k * D; J[1 + k].lddz = 3 * D;
-          J[1 + k].x = p->P_(s + "query1"); J[1 + k].ldx = D;
-        }
-      }
-      fill_group(p->wg_cross[l]);
-      {
-        auto& J = p->wg_cross[l].jobs;
-        const float* qin = p->P_(p->block_query(l));
-        J[0].dz = p->P_("dsum"); J[0].lddz = D; J[0].x = p->P_(s + "cres"); J[0].ldx = D;
-        if (p->I > 0) {
-          J[1].dz = p->P_("dqkv"); J[1].lddz = D; J[1].x = qin; J[1].ldx = D;   // dQ in dqkv[:, :D], ld D
-          for (int i = 0; i < p->I; ++i) {
-            const std::string si = std::to_string(i);
-            float* dkv = p->P_("dkv" + si);
-            J[2 + 2 * i].dz = dkv; J[2 + 2 * i].lddz = 2 * D;
-            J[2 + 2 * i].x = p->P_("fnenc" + si); J[2 + 2 * i].ldx = D;
-            J[3 + 2 * i].dz = dkv + D; J[3 + 2 * i].lddz = 2 * D;
-            J[3 + 2 * i].x = p->P_("fnenc" + si); J[3 + 2 * i].ldx = D;
-          }
-        } else {
-          float* dqkv = p->P_("dqkv");
-          J[1].dz = dqkv; J[1].lddz = 3 * D; J[1].x = qin; J[1].ldx = D;
-          J[2].dz = dqkv + D; J[2].lddz = 3 * D; J[2].x = qin; J[2].ldx = D;
-          J[3].dz = dqkv + 2 * D; J[3].lddz = 3 * D; J[3].x = qin; J[3].ldx = D;
-        }
-      }
-    }
-    auto upload_group = [&](WgradGroup& G) {
+  // point-reduction GEMM groups with real pointers
+  {
+    const size_t slab_need = p->slab_wgrad_floats;
+    build_groups(p);
+    if (p->slab_wgrad_floats != slab_need) return fail(GNOT_E_INVALID, "internal: slab size changed at bind");
+    for_each_group(p, [&](WgradGroup& G) {
       G.d_jobs = static_cast<WgradJob*>(put(G.jobs.data(), G.jobs.size() * sizeof(WgradJob)));
-      std::vector<int> pre(G.wave_prefix);
+      std::vector<int> pre(G.wg_prefix);
       pre.insert(pre.end(), G.red_prefix.begin(), G.red_prefix.end());
       int* d = static_cast<int*>(put(pre.data(), pre.size() * sizeof(int)));
-      G.d_wave_prefix = d;
+      G.d_wg_prefix = d;
       G.d_red_prefix = d + G.jobs.size();
-    };
-    upload_group(p->wg_out); upload_group(p->wg_x); upload_group(p->wg_gate);
-    for (auto& G : p->wg_fn) upload_group(G);
-    for (int l = 0; l < p->L; ++l) {
-      upload_group(p->wg_m1[l]); upload_group(p->wg_m2[l]);
-      upload_group(p->wg_self[l]); upload_group(p->wg_cross[l]);
-    }
+    });
   }
   if (cur > p->table_bytes) return fail(GNOT_E_INVALID, "internal: table overflow");
   GNOT_CK(hipMemcpy(tp, host.data(), cur, hipMemcpyHostToDevice));
@@ -833,6 +880,30 @@ struct Ctx {
   hipStream_t s;
 };
 
+// records a start/stop event pair around one launch when `kind` is the profiled kernel class
+struct ProfScope {
+  Ctx& c;
+  bool on = false;
+  size_t idx = 0;
+  ProfScope(Ctx& c_, const char* kind, double flops) : c(c_) {
+    gnot_plan* p = c.p;
+    if (p->prof_kind.empty() || p->prof_kind != kind) return;
+    while (p->prof_events.size() < p->prof_used + 2) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) return;
+      p->prof_events.push_back(e);
+    }
+    idx = p->prof_used;
+    p->prof_used += 2;
+    p->prof_flops += flops;
+    p->prof_launches += 1;
+    on = hipEventRecord(p->prof_events[idx], c.s) == hipSuccess;
+  }
+  ~ProfScope() {
+    if (on) (void)hipEventRecord(c.p->prof_events[idx + 1], c.s);
+  }
+};
+
 int run_linear(Ctx& c, const float* X, long ldx, int K, const Img& A, const float* bias, float* Y, long ldy,
                int NO, long P, int epi, int nsoft) {
   LinearArgs a{};
@@ -850,20 +921,12 @@ ChainArgs chain_args(gnot_plan* p, const ChainTable& T, long P) {
   return a;
 }
 
-int run_state(Ctx& c, const float* A, long lda, const float* Bv, long ldb, const float* w, long ldw,
-              const int4* chunks, int nchunks, const int* choff, float* state) {
-  gnot_plan* p = c.p;
-  AttnStateArgs a{};
-  a.A = A; a.lda = lda; a.Bv = Bv; a.ldb = ldb; a.w = w; a.ldw = ldw;
-  a.H = p->H; a.dh = p->dh; a.chunks = chunks; a.nchunks = nchunks;
-  a.slab = p->P_("slab_state"); a.sample_chunk_off = choff; a.B = p->B; a.state = state;
-  GNOT_CK(launch_attn_state(a, c.s));
-  return GNOT_OK;
-}
-
 int run_wgrad(Ctx& c, const WgradGroup& G) {
   if (G.jobs.empty()) return GNOT_OK;
-  GNOT_CK(launch_wgrad(G.d_jobs, G.d_wave_prefix, (int)G.jobs.size(), G.total_waves, G.d_red_prefix,
+  double fl = 0.0;
+  for (const auto& J : G.jobs) fl += 2.0 * J.P * (double)J.out * J.in;
+  ProfScope ps(c, G.jobs[0].state_dh > 0 ? "state" : "wgrad", fl);
+  GNOT_CK(launch_wgrad(G.d_jobs, G.d_wg_prefix, (int)G.jobs.size(), G.total_wgs, G.d_red_prefix,
                        G.total_red, c.p->P_("slab_wgrad"), c.s));
   return GNOT_OK;
 }
@@ -892,10 +955,8 @@ int attn_forward(Ctx& c, int l, bool cross, const float* q_in, float* res_out, f
       float* kv = p->P_(s + "ckv" + si);
       GNOT_RUN(run_linear(c, p->P_("fnenc" + si), D, D, A.kv[i], pbias + A.bkv[i], kv, 2 * D, 2 * D, p->Q[i],
                           EPI_STORE, D));
-      float* st = p->P_(s + "cstate" + si);
-      GNOT_RUN(run_state(c, kv, 2 * D, kv + D, 2 * D, nullptr, 0, p->d_fchunks[i], (int)p->fchunks[i].size(),
-                         p->d_fchunk_off[i], st));
-      ap.state[i] = st;
+      GNOT_RUN(run_wgrad(c, p->st_c[l][i]));
+      ap.state[i] = p->P_(s + "cstate" + si);
     }
     ap.q = q; ap.ldq = D; ap.nsrc = p->I; ap.chunks = p->d_qchunks; ap.nchunks = nq; ap.off = p->d_xoff;
     ap.H = p->H; ap.dh = p->dh; ap.res = res_out;
@@ -904,7 +965,7 @@ int attn_forward(Ctx& c, int l, bool cross, const float* q_in, float* res_out, f
     float* qkv = p->P_(cross ? s + "cq" : s + "sq");
     GNOT_RUN(run_linear(c, q_in, D, D, A.qkv, pbias + A.bqkv, qkv, 3 * D, 3 * D, P, EPI_STORE, 2 * D));
     float* st = p->P_(cross ? s + "cstate0" : s + "sstate");
-    GNOT_RUN(run_state(c, qkv + D, 3 * D, qkv + 2 * D, 3 * D, nullptr, 0, p->d_qchunks, nq, p->d_qchunk_off, st));
+    GNOT_RUN(run_wgrad(c, cross ? p->st_c[l][0] : p->st_s[l]));
     AttnApplyArgs ap{};
     ap.q = qkv; ap.ldq = 3 * D; ap.nsrc = 1; ap.state[0] = st; ap.chunks = p->d_qchunks; ap.nchunks = nq;
     ap.off = p->d_xoff; ap.H = p->H; ap.dh = p->dh; ap.res = res_out;
@@ -945,8 +1006,7 @@ int attn_backward(Ctx& c, int l, bool cross, const float* q_in) {
     for (int i = 0; i < p->I; ++i) {
       const std::string si = std::to_string(i);
       float* dst = p->P_("dstate" + si);
-      GNOT_RUN(run_state(c, q, D, p->P_("du" + si), D, p->P_("dden" + si), p->H, p->d_qchunks, nq,
-                         p->d_qchunk_off, dst));
+      GNOT_RUN(run_wgrad(c, p->dst_c[l][i]));
       const float* kv = p->P_(s + "ckv" + si);
       float* dkv = p->P_("dkv" + si);
       AttnKVBwdArgs kb{};
@@ -970,8 +1030,7 @@ int attn_backward(Ctx& c, int l, bool cross, const float* q_in) {
     ap.dden[0] = p->P_("dden0");
     GNOT_CK(launch_attn_apply_bwd(ap, c.s));
     float* dst = p->P_("dstate0");
-    GNOT_RUN(run_state(c, qkv, 3 * D, p->P_("du0"), D, p->P_("dden0"), p->H, p->d_qchunks, nq,
-                       p->d_qchunk_off, dst));
+    GNOT_RUN(run_wgrad(c, cross ? p->dst_c[l][0] : p->dst_s[l]));
     AttnKVBwdArgs kb{};
     kb.k = qkv + D; kb.v = qkv + 2 * D; kb.ldkv = 3 * D; kb.dstate = dst; kb.chunks = p->d_qchunks;
     kb.nchunks = nq; kb.H = p->H; kb.dh = p->dh; kb.dk = dqkv + D; kb.dv = dqkv + 2 * D; kb.lddkv = 3 * D;
@@ -1041,7 +1100,10 @@ extern "C" int gnot_forward(gnot_plan* p, const float* x, const float* theta, co
       a.X = p->P_(s + "a"); a.ldx = D; a.Y = p->P_("stage"); a.ldy = D; a.y_chain_stride = P * D;
       a.scores = p->P_("scores"); a.ldsc = (int)p->bufs["scores"].ld; a.mode = CH_MOE;
       if (tr) { a.save = p->P_(s + "m1save"); a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D; }
-      GNOT_CK(launch_chain_fwd(a, c.s));
+      {
+        ProfScope ps(c, "moe_fwd", 2.0 * E * P * NL * (double)D * D);
+        GNOT_CK(launch_chain_fwd(a, c.s));
+      }
       GNOT_CK(launch_moe_combine(qin, p->P_("stage"), P * D, E, p->P_(s + "query1"), P * D, c.s));
     }
     GNOT_RUN(attn_forward(c, l, false, p->P_(s + "query1"), p->P_(s + "sres"), p->P_(s + "bb")));
@@ -1050,7 +1112,10 @@ extern "C" int gnot_forward(gnot_plan* p, const float* x, const float* theta, co
       a.X = p->P_(s + "bb"); a.ldx = D; a.Y = p->P_("stage"); a.ldy = D; a.y_chain_stride = P * D;
       a.scores = p->P_("scores"); a.ldsc = (int)p->bufs["scores"].ld; a.mode = CH_MOE;
       if (tr) { a.save = p->P_(s + "m2save"); a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D; }
-      GNOT_CK(launch_chain_fwd(a, c.s));
+      {
+        ProfScope ps(c, "moe_fwd", 2.0 * E * P * NL * (double)D * D);
+        GNOT_CK(launch_chain_fwd(a, c.s));
+      }
       GNOT_CK(launch_moe_combine(p->P_(s + "query1"), p->P_("stage"), P * D, E, p->P_(s + "query2"), P * D, c.s));
     }
   }
@@ -1100,7 +1165,10 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
       a.save = p->P_(s + "m2save"); a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D;
       a.dz = dz; a.dz_layer_stride = P * D; a.dz_chain_stride = NL * P * D;
       a.dX = stage; a.lddx = D; a.dx_chain_stride = P * D;
-      GNOT_CK(launch_chain_bwd(a, c.s));
+      {
+        ProfScope ps(c, "moe_bwd", 2.0 * E * P * NL * (double)D * D);
+        GNOT_CK(launch_chain_bwd(a, c.s));
+      }
       GNOT_RUN(run_wgrad(c, p->wg_m2[l]));
       GNOT_CK(launch_moe_combine(nullptr, stage, P * D, E, p->P_("dsum"), P * D, c.s));
     }
@@ -1114,7 +1182,10 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
       a.save = p->P_(s + "m1save"); a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D;
       a.dz = dz; a.dz_layer_stride = P * D; a.dz_chain_stride = NL * P * D;
       a.dX = stage; a.lddx = D; a.dx_chain_stride = P * D;
-      GNOT_CK(launch_chain_bwd(a, c.s));
+      {
+        ProfScope ps(c, "moe_bwd", 2.0 * E * P * NL * (double)D * D);
+        GNOT_CK(launch_chain_bwd(a, c.s));
+      }
       GNOT_RUN(run_wgrad(c, p->wg_m1[l]));
       GNOT_CK(launch_moe_combine(nullptr, stage, P * D, E, p->P_("dsum"), P * D, c.s));
     }
@@ -1151,6 +1222,33 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
     GNOT_RUN(run_wgrad(c, p->wg_gate));
   }
   (void)E;
+  return GNOT_OK;
+}
+
+extern "C" int gnot_profile_enable(gnot_plan* p, const char* kind) {
+  if (!p) return fail(GNOT_E_INVALID, "null plan");
+  p->prof_kind = kind ? kind : "";
+  p->prof_used = 0;
+  p->prof_flops = 0.0;
+  p->prof_launches = 0;
+  return GNOT_OK;
+}
+
+extern "C" int gnot_profile_read(gnot_plan* p, double* ms_total, int64_t* launches, double* flops_total) {
+  if (!p) return fail(GNOT_E_INVALID, "null plan");
+  double ms = 0.0;
+  for (size_t k = 0; k + 1 < p->prof_used; k += 2) {
+    GNOT_CK(hipEventSynchronize(p->prof_events[k + 1]));
+    float t = 0.f;
+    GNOT_CK(hipEventElapsedTime(&t, p->prof_events[k], p->prof_events[k + 1]));
+    ms += t;
+  }
+  if (ms_total) *ms_total = ms;
+  if (launches) *launches = p->prof_launches;
+  if (flops_total) *flops_total = p->prof_flops;
+  p->prof_used = 0;
+  p->prof_flops = 0.0;
+  p->prof_launches = 0;
   return GNOT_OK;
 }
 

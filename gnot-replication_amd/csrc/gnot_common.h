@@ -103,6 +103,50 @@ GNOT_DEV void mm_tiles(const float4* __restrict__ Wp, const float (&in)[KT][4], 
   }
 }
 
+// ---- LDS-staged weight images ---------------------------------------------------------------
+// A layer's packed A-operand image (OT x KT tiles of 1 KiB) is copied into LDS by the whole
+// workgroup with global_load_lds (16 B per lane, one 1 KiB wave-instruction each, no VGPRs), then every
+// wave of the workgroup reads its fragments with ds_read_b128 (contiguous -> conflict free).  Images
+// larger than kLdsImageKB are processed in chunks of `och` output tiles.
+constexpr int kLdsImageKB = 64;
+
+constexpr int lds_och(int KT, int OT) {
+  int c = OT;
+  while (c > 1 && (c * KT > kLdsImageKB || OT % c != 0)) --c;
+  return c;
+}
+
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+typedef __attribute__((address_space(1))) const void* global_cvoid_ptr;
+
+// copy n4 float4 (a multiple of 64) from global to LDS; all threads of the workgroup call this
+GNOT_DEV void stage_image(float4* lds, const float4* __restrict__ g, int n4, int nwaves, int wave, int lane) {
+  for (int base = wave * WAVE; base < n4; base += nwaves * WAVE)
+    __builtin_amdgcn_global_load_lds((global_cvoid_ptr)(g + base + lane), (lds_void_ptr)(lds + base), 16, 0, 0);
+}
+
+// acc[o] (o < OT) += W x in  with W (OT x KT tiles, packed) streamed through the LDS buffer `lds`
+// (capacity >= lds_och(KT,OT)*KT*64 float4).  Contains __syncthreads(): call uniformly.
+template <int KT, int OT>
+GNOT_DEV void mm_tiles_lds(const float4* __restrict__ Wg, float4* lds, const float (&in)[KT][4], f32x4 (&acc)[OT],
+                           int nwaves, int wave, int lane) {
+  constexpr int OCH = lds_och(KT, OT);
+#pragma unroll
+  for (int c = 0; c < OT / OCH; ++c) {
+    __syncthreads();                                   // previous readers of lds are done
+    stage_image(lds, Wg + c * OCH * KT * WAVE, OCH * KT * WAVE, nwaves, wave, lane);
+    __syncthreads();                                   // drains the LDS-DMA (vmcnt(0)) + barrier
+#pragma unroll
+    for (int T = 0; T < KT; ++T) {
+      float4 w[OCH];
+#pragma unroll
+      for (int o = 0; o < OCH; ++o) w[o] = lds[(o * KT + T) * WAVE + lane];
+#pragma unroll
+      for (int o = 0; o < OCH; ++o) acc[c * OCH + o] = mfma_k16(w[o], in[T], acc[c * OCH + o]);
+    }
+  }
+}
+
 template <int OT>
 GNOT_DEV void init_bias(f32x4 (&acc)[OT], const float* __restrict__ bias, int lane) {
   const int g = lane >> 4;

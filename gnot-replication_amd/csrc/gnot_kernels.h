@@ -75,39 +75,30 @@ struct ChainArgs {
 hipError_t launch_chain_fwd(const ChainArgs& a, hipStream_t s);
 hipError_t launch_chain_bwd(const ChainArgs& a, hipStream_t s);
 
-// ------------------------------------------------------------------ weight gradients (wgrad.hip)
+// ------------------------------------------------------------------ point-reduction GEMM (wgrad.hip)
+// C[out, in] = sum_p dz[p, :out]^T x[p, :in] over a point range, plus column sums of dz.
 struct WgradJob {
-  const float* dz; long lddz;        // [P, out]   (columns [0, out))
-  const float* x;  long ldx;         // [P, in]
-  int x_gelu;                        // 1: the layer input is gelu(x)
+  const float* dz; long lddz;        // A rows [P, out]
+  const float* x;  long ldx;         // B rows [P, in]
+  int x_gelu;                        // 1: B = gelu(x) (x is a saved pre-activation)
   int out, in;
-  float* dW;                         // [out, in] row-major (parameter gradient layout)
-  float* db;                         // [out] or null
+  float* dW;                         // [out, in] row-major, or the state [H][dh*dh + dh] (state_dh > 0)
+  float* db;                         // [out] column sums of A, or null
+  const float* w; long ldw; int wdh; // optional per-(point, column/wdh) weight of the column sums
+  int state_dh;                      // > 0: keep only dh x dh diagonal blocks, state layout
+  int diag_only;                     // compute only the diagonal 128x128 tiles
   int P;
-  int tiles_o, tiles_i;              // 32x32 output tiles
+  int tiles_o, tiles_i;              // 128x128 output tiles
   int splits;                        // split-K count over points
-  long slab_off;                     // offset (floats) of this job's partial slabs in the workspace
+  long slab_off;                     // offset (floats) of this job's partial slabs
   int accumulate;                    // 1: dW += result
 };
-hipError_t launch_wgrad(const WgradJob* jobs_dev, const int* wave_prefix_dev, int njobs, int total_waves,
+// one workgroup per (job, tile, split); wg_prefix / red_prefix: per-job prefix sums of workgroups and
+// of reduce elements (ntile * 128 * 129)
+hipError_t launch_wgrad(const WgradJob* jobs_dev, const int* wg_prefix_dev, int njobs, int total_wgs,
                         const int* red_prefix_dev, int total_red, float* slab, hipStream_t s);
 
 // ------------------------------------------------------------------ attention (attn.hip)
-struct Segment { int b; int start; int len; int chunk0; };   // one point chunk of one sample
-struct AttnStateArgs {
-  const float* A; long lda;          // [P, d] (head h at columns h*dh)
-  const float* Bv; long ldb;
-  const float* w; long ldw;          // optional [P, H] weights for z (null -> 1)
-  int H, dh;
-  const int4* chunks;                // (b, start, len, -) per chunk
-  int nchunks;
-  float* slab;                       // [nchunks][H][dh*dh + dh]
-  const int* sample_chunk_off;       // [B+1] chunk ranges per sample
-  int B;
-  float* state;                      // [B][H][dh*dh + dh]
-};
-hipError_t launch_attn_state(const AttnStateArgs& a, hipStream_t s);
-
 struct AttnApplyArgs {
   const float* q; long ldq;          // post-softmax q, point-major
   int nsrc;                          // number of (S, z) sets to average (I, or 1 for self)

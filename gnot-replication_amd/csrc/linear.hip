@@ -15,7 +15,8 @@ namespace gnot {
 template <int D>
 __global__ void __launch_bounds__(256) linear_kernel(LinearArgs a) {
   constexpr int KT = D / 16;
-  constexpr int OC = (D / 16) < 8 ? (D / 16) : 8;
+  constexpr int OC = lds_och(KT, (D / 16) < 8 ? (D / 16) : 8);   // output tiles per chunk (<= 64 KiB of W)
+  __shared__ __attribute__((aligned(16))) float4 wlds[OC * KT * WAVE];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const long p = ((long)blockIdx.x * 4 + wave) * 16 + (lane & 15);
@@ -36,7 +37,7 @@ __global__ void __launch_bounds__(256) linear_kernel(LinearArgs a) {
   for (int c = 0; c < nchunks; ++c) {
     f32x4 acc[OC];
     init_bias<OC>(acc, a.bias ? a.bias + c * 16 * OC : nullptr, lane);
-    mm_tiles<KT, OC>(a.Wp + (long)c * OC * KT * WAVE, in, acc, lane);
+    mm_tiles_lds<KT, OC>(a.Wp + (long)c * OC * KT * WAVE, wlds, in, acc, 4, wave, lane);
     float h[OC][4];
     acc_to_regs<OC>(acc, h);
     if (c * 16 * OC < a.nsoft) softmax_heads<OC>(h, a.dh);

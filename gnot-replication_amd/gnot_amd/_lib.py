@@ -26,7 +26,8 @@ EXPORTS = [
     "gnot_plan_create", "gnot_plan_destroy", "gnot_plan_num_linears", "gnot_plan_linear_dims",
     "gnot_plan_bind_params", "gnot_plan_set_batch", "gnot_plan_workspace_bytes",
     "gnot_plan_bind_workspace", "gnot_plan_grad_offsets", "gnot_pack_weights", "gnot_forward",
-    "gnot_backward", "gnot_debug_buffer", "gnot_last_error", "gnot_version",
+    "gnot_backward", "gnot_profile_enable", "gnot_profile_read", "gnot_debug_buffer", "gnot_last_error",
+    "gnot_version",
 ]
 
 
@@ -56,6 +57,9 @@ def _declare(lib):
     lib.gnot_pack_weights.argtypes = [P, P]
     lib.gnot_forward.argtypes = [P, P, P, ctypes.POINTER(P), P, P]
     lib.gnot_backward.argtypes = [P, P, P]
+    lib.gnot_profile_enable.argtypes = [P, ctypes.c_char_p]
+    lib.gnot_profile_read.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64),
+                                      ctypes.POINTER(ctypes.c_double)]
     lib.gnot_debug_buffer.argtypes = [P, ctypes.c_char_p, ctypes.POINTER(P), ctypes.POINTER(i64)]
     lib.gnot_last_error.restype = ctypes.c_char_p
     lib.gnot_last_error.argtypes = []

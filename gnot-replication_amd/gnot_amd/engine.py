@@ -36,6 +36,8 @@ class Engine:
         self.geom = None
         self.ws = None
         self.grad_views = None
+        self.grad_arena = None     # flat fp32 view of every parameter gradient (one buffer)
+        self.grad_hook = None      # optional callable(grad_arena) run after the backward kernels
         self.fwd_token = 0
 
     def __del__(self):
@@ -78,6 +80,7 @@ class Engine:
         _lib.check(self.lib.gnot_plan_bind_workspace(self.plan, self.ws.data_ptr(), self.ws.numel()))
         self.geom = geom
         self.grad_views = None
+        self.grad_arena = None
         if training:
             n = len(self.dims)
             offs = (ctypes.c_int64 * (2 * n))()
@@ -90,6 +93,8 @@ class Engine:
                 bo = base // 4 + offs[2 * k + 1]
                 views.append((wsf[wo:wo + o * i].view(o, i), wsf[bo:bo + o]))
             self.grad_views = views
+            last_o = self.dims[-1][0]
+            self.grad_arena = wsf[base // 4: base // 4 + offs[2 * n - 1] + last_o]
 
     def debug_ptr(self, name):
         ptr = ctypes.c_void_p()
@@ -105,6 +110,15 @@ class Engine:
         ld = ld if ld > 0 else cols
         return wsf[off:off + rows * ld].view(rows, ld)[:, :cols].clone()
 
+    def profile_enable(self, kind):
+        _lib.check(self.lib.gnot_profile_enable(self.plan, (kind or "").encode()))
+
+    def profile_read(self):
+        """(device ms summed over launches, launches, algorithmic FLOPs) since enable/last read."""
+        ms, n, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
+        _lib.check(self.lib.gnot_profile_read(self.plan, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl)))
+        return ms.value, n.value, fl.value
+
     # ---------------------------------------------------------------- compute
     def stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -119,4 +133,6 @@ class Engine:
 
     def backward(self, dout):
         _lib.check(self.lib.gnot_backward(self.plan, dout.data_ptr(), self.stream()))
+        if self.grad_hook is not None:
+            self.grad_hook(self.grad_arena)     # e.g. ONE all-reduce of all gradients (sample-DP)
         return self.grad_views

@@ -98,6 +98,14 @@ int gnot_forward(gnot_plan* plan, const float* x, const float* theta, const floa
  * (overwritten) into the gradient arena. */
 int gnot_backward(gnot_plan* plan, const float* dout, void* stream);
 
+/* Live kernel timing for the bench's roofline: while enabled, every launch of kernel class `kind`
+ * ("moe_fwd" fused expert chains forward, "moe_bwd" their backward, "wgrad" weight-gradient GEMMs;
+ * "" disables) is bracketed by hipEvents on its stream.  gnot_profile_read synchronizes on those
+ * events and returns the summed device time, the launch count and the algorithmic FLOPs of those
+ * launches, then resets the counters. */
+int gnot_profile_enable(gnot_plan* plan, const char* kind);
+int gnot_profile_read(gnot_plan* plan, double* ms_total, int64_t* launches, double* flops_total);
+
 /* Debug/test hook: device pointer + row stride (floats) of a named intermediate buffer
  * ("scores", "query0", "out_h0", ...); returns GNOT_E_INVALID for unknown names. */
 int gnot_debug_buffer(const gnot_plan* plan, const char* name, float** ptr, int64_t* ld);

@@ -53,3 +53,25 @@ def test_padding_changes_real_outputs():
     xp = np.concatenate([fx["x"][b0], np.zeros((9, fx["x"].shape[1]))])
     outp, _ = O.gnot_forward_backward(fx["params"], fx["cfg"], xp, np.array([0, n + 9]), fx["theta"][:1], fs, fo)
     assert np.abs(outp[:n] - out0).max() > 1e-10
+
+
+@pytest.mark.parametrize("name", ["cross1_sharp", "self_only_pad", "cross2_packed"])
+def test_torch_port_matches_fixtures(name):
+    """The stock-torch CPU port timed as bench.py's cpu_baseline computes the reference's numbers."""
+    import torch
+    from oracle import torch_port
+    fx = load(name)
+    cfg = fx["cfg"]
+    p = {k: torch.from_numpy(v).clone().requires_grad_(True) for k, v in fx["params"].items()}
+    outs = []
+    for b in range(len(fx["x_off"]) - 1):
+        s, e = fx["x_off"][b], fx["x_off"][b + 1]
+        x = torch.from_numpy(fx["x"][s:e])[None]
+        fns = [torch.from_numpy(f[o[b]:o[b + 1]])[None] for f, o in zip(fx["fns"], fx["fn_offs"])]
+        o = torch_port.gnot_forward(p, cfg, x, torch.from_numpy(fx["theta"][b:b + 1]), fns)[0]
+        (o * torch.from_numpy(fx["G"][s:e])).sum().backward()
+        outs.append(o.detach().numpy())
+    grads = {k: v.grad.numpy() for k, v in p.items()}
+    errs = check_parity(np.concatenate(outs), grads, fx, rtol=1e-9, slack=0.0)
+    errs = [e for e in errs if not any(t in e for t in ("key", "query"))]
+    assert not errs, errs
