@@ -141,7 +141,7 @@ def main():
     model = GNOT(*[m[k] for k in ("input_dim", "theta_dim", "input_func_dim", "out_dim", "n_attn_layers",
                                   "n_attn_hidden_dim", "n_mlp_num_layers", "n_mlp_hidden_dim",
                                   "n_input_hidden_dim", "n_expert", "n_head", "n_input_functions")]).to(device)
-    opt = torch.optim.AdamW(model.parameters(), lr=1e-3)          # main.py:50-51
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-3, fused=True)   # main.py:50-51 (fused kernel)
     x, x_off, theta, fns, fn_offs, y, seg = make_batch(w, 100 + rank, device)
     B = w["B"]
     eng = model.engine()

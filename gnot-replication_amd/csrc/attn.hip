@@ -19,6 +19,39 @@
 
 namespace gnot {
 
+// u = x M  for a row vector x[DH] and a row-major DH x DH matrix M in LDS (float4 row reads)
+template <int DH>
+GNOT_DEV void rowvec_times_mat(const float (&x)[DH], const float* M, float (&u)[DH]) {
+#pragma unroll
+  for (int j = 0; j < DH; ++j) u[j] = 0.f;
+#pragma unroll
+  for (int k = 0; k < DH; ++k) {
+#pragma unroll
+    for (int j = 0; j < DH; j += 4) {
+      const float4 m = *reinterpret_cast<const float4*>(M + k * DH + j);
+      u[j] = fmaf(x[k], m.x, u[j]);
+      u[j + 1] = fmaf(x[k], m.y, u[j + 1]);
+      u[j + 2] = fmaf(x[k], m.z, u[j + 2]);
+      u[j + 3] = fmaf(x[k], m.w, u[j + 3]);
+    }
+  }
+}
+
+// x . row  for a row of DH floats in LDS
+template <int DH>
+GNOT_DEV float dot_row(const float (&x)[DH], const float* row) {
+  float a = 0.f, b = 0.f;
+#pragma unroll
+  for (int j = 0; j < DH; j += 4) {
+    const float4 m = *reinterpret_cast<const float4*>(row + j);
+    a = fmaf(x[j], m.x, a);
+    b = fmaf(x[j + 1], m.y, b);
+    a = fmaf(x[j + 2], m.z, a);
+    b = fmaf(x[j + 3], m.w, b);
+  }
+  return a + b;
+}
+
 // ---------------------------------------------------------------- apply (forward)
 template <int DH>
 __global__ void __launch_bounds__(256) attn_apply_fwd_kernel(AttnApplyArgs a) {
@@ -36,9 +69,11 @@ __global__ void __launch_bounds__(256) attn_apply_fwd_kernel(AttnApplyArgs a) {
   const long Nb = a.off[b + 1] - off_b;
   const int d = H * DH;
   const float inv_nsrc = 1.0f / (float)a.nsrc;
+  // head-major work order: consecutive lanes take consecutive points of the SAME head, so the
+  // per-head state reads below are LDS broadcasts
   for (int idx = threadIdx.x; idx < ch.z * H; idx += 256) {
-    const long n = ch.y + idx / H;     // global point index
-    const int h = idx % H;
+    const int h = idx / ch.z;
+    const long n = ch.y + idx % ch.z;  // global point index
     float q[DH], os[DH];
 #pragma unroll
     for (int j = 0; j < DH; j += 4) {
@@ -54,12 +89,7 @@ __global__ void __launch_bounds__(256) attn_apply_fwd_kernel(AttnApplyArgs a) {
 #pragma unroll
       for (int k = 0; k < DH; ++k) den = fmaf(q[k], z[k], den);
       float u[DH];
-#pragma unroll
-      for (int j = 0; j < DH; ++j) u[j] = 0.f;
-#pragma unroll
-      for (int k = 0; k < DH; ++k)
-#pragma unroll
-        for (int j = 0; j < DH; ++j) u[j] = fmaf(q[k], S[k * DH + j], u[j]);
+      rowvec_times_mat<DH>(q, S, u);
       const float inv = 1.0f / den;
 #pragma unroll
       for (int j = 0; j < DH; ++j) os[j] = fmaf(u[j], inv, os[j]);
@@ -91,8 +121,8 @@ __global__ void __launch_bounds__(256) attn_apply_bwd_kernel(AttnApplyArgs a) {
   const int d = H * DH;
   const float inv_nsrc = 1.0f / (float)a.nsrc;
   for (int idx = threadIdx.x; idx < ch.z * H; idx += 256) {
-    const long n = ch.y + idx / H;
-    const int h = idx % H;
+    const int h = idx / ch.z;          // head-major (LDS broadcast of the state)
+    const long n = ch.y + idx % ch.z;
     float q[DH], dO[DH], dq[DH];
     const float* src = a.dres + off_b * d + ((long)h * Nb + (n - off_b)) * DH;
 #pragma unroll
@@ -111,12 +141,7 @@ __global__ void __launch_bounds__(256) attn_apply_bwd_kernel(AttnApplyArgs a) {
 #pragma unroll
       for (int k = 0; k < DH; ++k) den = fmaf(q[k], z[k], den);
       float u[DH];
-#pragma unroll
-      for (int j = 0; j < DH; ++j) u[j] = 0.f;
-#pragma unroll
-      for (int k = 0; k < DH; ++k)
-#pragma unroll
-        for (int j = 0; j < DH; ++j) u[j] = fmaf(q[k], S[k * DH + j], u[j]);
+      rowvec_times_mat<DH>(q, S, u);
       const float inv = 1.0f / den;
       // o = u/den ; du = dO/den ; dden = -(dO . o)/den
       float dot = 0.f;
@@ -128,12 +153,7 @@ __global__ void __launch_bounds__(256) attn_apply_bwd_kernel(AttnApplyArgs a) {
       for (int j = 0; j < DH; ++j) du[j] = dO[j] * inv;
       // dq += du S^T + dden z
 #pragma unroll
-      for (int k = 0; k < DH; ++k) {
-        float acc = dden * z[k];
-#pragma unroll
-        for (int j = 0; j < DH; ++j) acc = fmaf(du[j], S[k * DH + j], acc);
-        dq[k] += acc;
-      }
+      for (int k = 0; k < DH; ++k) dq[k] = fmaf(dden, z[k], dq[k] + dot_row<DH>(du, S + k * DH));
       float* dup = a.du[sidx] + n * a.lddu + h * DH;
 #pragma unroll
       for (int j = 0; j < DH; j += 4)
@@ -164,8 +184,8 @@ __global__ void __launch_bounds__(256) attn_kv_bwd_kernel(AttnKVBwdArgs a) {
   for (int i = threadIdx.x; i < per; i += 256) smem[i] = a.dstate[(long)b * per + i];
   __syncthreads();
   for (int idx = threadIdx.x; idx < ch.z * H; idx += 256) {
-    const long m = ch.y + idx / H;
-    const int h = idx % H;
+    const int h = idx / ch.z;          // head-major (LDS broadcast of dS)
+    const long m = ch.y + idx % ch.z;
     const float* dS = smem + h * (DH * DH + DH);
     const float* dz = dS + DH * DH;
     float k[DH], v[DH];
@@ -178,18 +198,8 @@ __global__ void __launch_bounds__(256) attn_kv_bwd_kernel(AttnKVBwdArgs a) {
     }
     float dk[DH], dv[DH];
 #pragma unroll
-    for (int i = 0; i < DH; ++i) {
-      float acc = dz[i];
-#pragma unroll
-      for (int j = 0; j < DH; ++j) acc = fmaf(v[j], dS[i * DH + j], acc);
-      dk[i] = acc;
-    }
-#pragma unroll
-    for (int j = 0; j < DH; ++j) dv[j] = 0.f;
-#pragma unroll
-    for (int i = 0; i < DH; ++i)
-#pragma unroll
-      for (int j = 0; j < DH; ++j) dv[j] = fmaf(k[i], dS[i * DH + j], dv[j]);
+    for (int i = 0; i < DH; ++i) dk[i] = dz[i] + dot_row<DH>(v, dS + i * DH);
+    rowvec_times_mat<DH>(k, dS, dv);
     float kdk = 0.f;
 #pragma unroll
     for (int i = 0; i < DH; ++i) kdk = fmaf(k[i], dk[i], kdk);

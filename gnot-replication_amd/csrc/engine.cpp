@@ -424,7 +424,8 @@ static void finish_group(gnot_plan* p, WgradGroup& G) {
   G.slab_floats = 0;
   int wg = 0, red = 0;
   for (auto& J : G.jobs) {
-    const long maxs = std::max<long>(1, (J.P + kMinSplitPoints - 1) / kMinSplitPoints);
+    const long minpts = J.state_dh > 0 ? 32 : kMinSplitPoints;   // state reductions: tiny, latency-bound
+    const long maxs = std::max<long>(1, (J.P + minpts - 1) / minpts);
     J.splits = (int)std::min<long>(std::min<long>(want, maxs), 256);
     const int nt = J.diag_only ? J.tiles_o : J.tiles_o * J.tiles_i;
     J.slab_off = (long)G.slab_floats;

@@ -41,10 +41,31 @@ GNOT_DEV f32x4 mfma_k16(const float4 w, const float (&x)[4], f32x4 c) {
 constexpr float kSqrt1_2 = 0.70710678118654752440f;
 constexpr float kInvSqrt2Pi = 0.39894228040143267794f;
 
-// nn.GELU() (exact erf), reference model.py:10,13
-GNOT_DEV float gelu(float x) { return 0.5f * x * (1.0f + erff(x * kSqrt1_2)); }
+// nn.GELU() (exact-erf form, reference model.py:10,13): gelu(x) = x * Phi(x), Phi(x) = (1 + erf(x/sqrt2))/2.
+// erf by Abramowitz-Stegun 7.1.26 (|error| <= 1.5e-7, below fp32 rounding of the result for |x| > 1):
+// one v_rcp, one v_exp and 5 FMAs instead of ocml erff's two-branch ~40-instruction sequence.  The
+// e^{-x^2/2} factor is shared with the derivative gelu'(x) = Phi(x) + x phi(x).
+GNOT_DEV void gelu_parts(float x, float& Phi, float& e) {
+  const float u = fabsf(x) * kSqrt1_2;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, u, 1.0f));
+  float poly = fmaf(t, 1.061405429f, -1.453152027f);
+  poly = fmaf(t, poly, 1.421413741f);
+  poly = fmaf(t, poly, -0.284496736f);
+  poly = fmaf(t, poly, 0.254829592f);
+  poly *= t;
+  e = __expf(-u * u);                       // = exp(-x^2 / 2)
+  const float erf_abs = fmaf(-poly, e, 1.0f);
+  Phi = 0.5f + 0.5f * copysignf(erf_abs, x);
+}
+GNOT_DEV float gelu(float x) {
+  float Phi, e;
+  gelu_parts(x, Phi, e);
+  return x * Phi;
+}
 GNOT_DEV float gelu_grad(float x) {
-  return 0.5f * (1.0f + erff(x * kSqrt1_2)) + x * kInvSqrt2Pi * __expf(-0.5f * x * x);
+  float Phi, e;
+  gelu_parts(x, Phi, e);
+  return fmaf(x * kInvSqrt2Pi, e, Phi);
 }
 
 GNOT_DEV float shfl_xor(float v, int m) { return __shfl_xor(v, m, 64); }

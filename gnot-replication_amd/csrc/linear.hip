@@ -33,8 +33,9 @@ __global__ void __launch_bounds__(256) linear_kernel(LinearArgs a) {
       for (int r = 0; r < 4; ++r) in[T][r] += t[T][r];
   }
 
+  // grid.y splits the output chunks over workgroups (more parallelism at small point counts)
   const int nchunks = a.NO / (16 * OC);
-  for (int c = 0; c < nchunks; ++c) {
+  for (int c = blockIdx.y; c < nchunks; c += gridDim.y) {
     f32x4 acc[OC];
     init_bias<OC>(acc, a.bias ? a.bias + c * 16 * OC : nullptr, lane);
     mm_tiles_lds<KT, OC>(a.Wp + (long)c * OC * KT * WAVE, wlds, in, acc, 4, wave, lane);
@@ -56,7 +57,9 @@ __global__ void __launch_bounds__(256) linear_kernel(LinearArgs a) {
 
 hipError_t launch_linear(const LinearArgs& a, int D, hipStream_t s) {
   if (a.P <= 0) return hipSuccess;
-  const dim3 grid((a.P + 63) / 64), block(256);
+  const int oc = lds_och(D / 16, D / 16 < 8 ? D / 16 : 8);   // == the kernel's OC
+  const int nchunks = a.NO / (16 * oc);
+  const dim3 grid((a.P + 63) / 64, nchunks), block(256);
   switch (D) {
     case 32: hipLaunchKernelGGL(linear_kernel<32>, grid, block, 0, s, a); break;
     case 48: hipLaunchKernelGGL(linear_kernel<48>, grid, block, 0, s, a); break;

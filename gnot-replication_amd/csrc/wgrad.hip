@@ -199,8 +199,15 @@ __global__ void __launch_bounds__(256) pgemm_reduce_kernel(const WgradJob* __res
   if (J.state_dh > 0 && !isdb && (row / J.state_dh) != (col / J.state_dh)) return;
   const float* S = slab + J.slab_off + (long)tile * (kTile * (kTile + 1)) + rl * (kTile + 1) + cl;
   const long sstride = (long)ntile * (kTile * (kTile + 1));
-  float s = 0.f;
-  for (int k = 0; k < J.splits; ++k) s += S[k * sstride];
+  // 8 independent partial sums keep 8 slab loads in flight (the loop is latency-bound otherwise);
+  // the combination order is fixed, so the result is still deterministic
+  float part[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int k = 0;
+  for (; k + 8 <= J.splits; k += 8)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) part[u] += S[(long)(k + u) * sstride];
+  for (; k < J.splits; ++k) part[0] += S[(long)k * sstride];
+  const float s = ((part[0] + part[1]) + (part[2] + part[3])) + ((part[4] + part[5]) + (part[6] + part[7]));
   float* dst;
   if (J.state_dh > 0) {
     const int dh = J.state_dh, hh = row / dh, i = row % dh;

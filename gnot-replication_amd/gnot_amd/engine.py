@@ -87,12 +87,14 @@ class Engine:
             _lib.check(self.lib.gnot_plan_grad_offsets(self.plan, offs))
             base = self.debug_ptr("grads")[0] - self.ws.data_ptr()
             wsf = self.ws[: (self.ws.numel() // 4) * 4].view(torch.float32)
-            views = []
+            views, layout = [], []
             for k, (o, i) in enumerate(self.dims):
                 wo = base // 4 + offs[2 * k]
                 bo = base // 4 + offs[2 * k + 1]
                 views.append((wsf[wo:wo + o * i].view(o, i), wsf[bo:bo + o]))
+                layout.append((offs[2 * k], offs[2 * k + 1], (o, i), o))
             self.grad_views = views
+            self.grad_layout = layout          # offsets relative to the arena start
             last_o = self.dims[-1][0]
             self.grad_arena = wsf[base // 4: base // 4 + offs[2 * n - 1] + last_o]
 

@@ -97,14 +97,16 @@ class _GNOTFunction(torch.autograd.Function):
         if eng.fwd_token != ctx.token:
             raise RuntimeError("gnot_amd keeps the activations of the most recent forward only; "
                                "backward must follow its own forward")
-        views = eng.backward(dout.contiguous().float())
-        grads = []
-        for w, b in views:
-            grads += [w.clone(), b.clone()]
+        eng.backward(dout.contiguous().float())
+        # ONE copy of the whole gradient arena (the workspace is reused by the next step); every
+        # parameter gradient is a view of that fresh buffer
+        flat = eng.grad_arena.clone()
+        ws, bs = [], []
+        for off_w, off_b, shape_w, nb in eng.grad_layout:
+            ws.append(flat[off_w:off_w + shape_w[0] * shape_w[1]].view(shape_w))
+            bs.append(flat[off_b:off_b + nb])
         # params were passed as (all weights..., all biases...)
-        n = len(views)
-        ordered = [grads[2 * k] for k in range(n)] + [grads[2 * k + 1] for k in range(n)]
-        return (None, None, None, None, None, *ordered)
+        return (None, None, None, None, None, *ws, *bs)
 
 
 class GNOT(nn.Module):
