@@ -10,8 +10,9 @@
 // at flat offset off_b*d + (h*N_b + n)*dh + j, and fc_out reads that buffer as plain rows.
 //
 // Kernels here:
-//   attn_apply_fwd / attn_apply_bwd  one thread per (point, head), per-sample (S, z) staged in LDS.
-//   attn_kv_bwd  dK, dV from (dS, dz) per (source point, head).
+//   attn_apply_fwd / attn_apply_bwd  grid (64-point segment, head): one wave, one thread per point,
+//                the head's (S, z) of every source staged in LDS and read as broadcasts.
+//   attn_kv_bwd  dK, dV from (dS, dz) per (source point, head), same geometry.
 // The cross-point reductions themselves (S, z forward; dS, dz backward) are point-reduction GEMMs
 // on the MFMA path (wgrad.hip, state jobs), one job per sample.
 #include "gnot_common.h"
@@ -54,26 +55,26 @@ GNOT_DEV float dot_row(const float (&x)[DH], const float* row) {
 
 // ---------------------------------------------------------------- apply (forward)
 template <int DH>
-__global__ void __launch_bounds__(256) attn_apply_fwd_kernel(AttnApplyArgs a) {
+__global__ void __launch_bounds__(64) attn_apply_fwd_kernel(AttnApplyArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int4 ch = a.chunks[blockIdx.x];
   const int b = ch.x;
   const int H = a.H;
-  const int per = H * (DH * DH + DH);
-  for (int i = threadIdx.x; i < a.nsrc * per; i += 256) {
-    const int sidx = i / per, e = i % per;
-    smem[i] = a.state[sidx][(long)b * per + e];
+  const int h = blockIdx.y;                 // one wave = up to 64 points of ONE head: LDS broadcasts
+  constexpr int ph = DH * DH + DH;
+  const int per = H * ph;
+  for (int i = threadIdx.x; i < a.nsrc * ph; i += 64) {
+    const int sidx = i / ph, e = i % ph;
+    smem[i] = a.state[sidx][(long)b * per + h * ph + e];
   }
   __syncthreads();
+  if ((int)threadIdx.x >= ch.z) return;
   const long off_b = a.off[b];
   const long Nb = a.off[b + 1] - off_b;
   const int d = H * DH;
   const float inv_nsrc = 1.0f / (float)a.nsrc;
-  // head-major work order: consecutive lanes take consecutive points of the SAME head, so the
-  // per-head state reads below are LDS broadcasts
-  for (int idx = threadIdx.x; idx < ch.z * H; idx += 256) {
-    const int h = idx / ch.z;
-    const long n = ch.y + idx % ch.z;  // global point index
+  {
+    const long n = ch.y + threadIdx.x;  // global point index
     float q[DH], os[DH];
 #pragma unroll
     for (int j = 0; j < DH; j += 4) {
@@ -83,7 +84,7 @@ __global__ void __launch_bounds__(256) attn_apply_fwd_kernel(AttnApplyArgs a) {
 #pragma unroll
     for (int j = 0; j < DH; ++j) os[j] = 0.f;
     for (int sidx = 0; sidx < a.nsrc; ++sidx) {
-      const float* S = smem + sidx * per + h * (DH * DH + DH);
+      const float* S = smem + sidx * ph;
       const float* z = S + DH * DH;
       float den = 0.f;
 #pragma unroll
@@ -105,24 +106,26 @@ __global__ void __launch_bounds__(256) attn_apply_fwd_kernel(AttnApplyArgs a) {
 
 // ---------------------------------------------------------------- apply (backward)
 template <int DH>
-__global__ void __launch_bounds__(256) attn_apply_bwd_kernel(AttnApplyArgs a) {
+__global__ void __launch_bounds__(64) attn_apply_bwd_kernel(AttnApplyArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int4 ch = a.chunks[blockIdx.x];
   const int b = ch.x;
   const int H = a.H;
-  const int per = H * (DH * DH + DH);
-  for (int i = threadIdx.x; i < a.nsrc * per; i += 256) {
-    const int sidx = i / per, e = i % per;
-    smem[i] = a.state[sidx][(long)b * per + e];
+  const int h = blockIdx.y;
+  constexpr int ph = DH * DH + DH;
+  const int per = H * ph;
+  for (int i = threadIdx.x; i < a.nsrc * ph; i += 64) {
+    const int sidx = i / ph, e = i % ph;
+    smem[i] = a.state[sidx][(long)b * per + h * ph + e];
   }
   __syncthreads();
+  if ((int)threadIdx.x >= ch.z) return;
   const long off_b = a.off[b];
   const long Nb = a.off[b + 1] - off_b;
   const int d = H * DH;
   const float inv_nsrc = 1.0f / (float)a.nsrc;
-  for (int idx = threadIdx.x; idx < ch.z * H; idx += 256) {
-    const int h = idx / ch.z;          // head-major (LDS broadcast of the state)
-    const long n = ch.y + idx % ch.z;
+  {
+    const long n = ch.y + threadIdx.x;
     float q[DH], dO[DH], dq[DH];
     const float* src = a.dres + off_b * d + ((long)h * Nb + (n - off_b)) * DH;
 #pragma unroll
@@ -135,7 +138,7 @@ __global__ void __launch_bounds__(256) attn_apply_bwd_kernel(AttnApplyArgs a) {
 #pragma unroll
     for (int j = 0; j < DH; ++j) dO[j] = dq[j] * inv_nsrc;
     for (int sidx = 0; sidx < a.nsrc; ++sidx) {
-      const float* S = smem + sidx * per + h * (DH * DH + DH);
+      const float* S = smem + sidx * ph;
       const float* z = S + DH * DH;
       float den = 0.f;
 #pragma unroll
@@ -175,18 +178,20 @@ __global__ void __launch_bounds__(256) attn_apply_bwd_kernel(AttnApplyArgs a) {
 
 // ---------------------------------------------------------------- K/V backward
 template <int DH>
-__global__ void __launch_bounds__(256) attn_kv_bwd_kernel(AttnKVBwdArgs a) {
+__global__ void __launch_bounds__(64) attn_kv_bwd_kernel(AttnKVBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int4 ch = a.chunks[blockIdx.x];
   const int b = ch.x;
   const int H = a.H;
-  const int per = H * (DH * DH + DH);
-  for (int i = threadIdx.x; i < per; i += 256) smem[i] = a.dstate[(long)b * per + i];
+  const int h = blockIdx.y;
+  constexpr int ph = DH * DH + DH;
+  const int per = H * ph;
+  for (int i = threadIdx.x; i < ph; i += 64) smem[i] = a.dstate[(long)b * per + h * ph + i];
   __syncthreads();
-  for (int idx = threadIdx.x; idx < ch.z * H; idx += 256) {
-    const int h = idx / ch.z;          // head-major (LDS broadcast of dS)
-    const long m = ch.y + idx % ch.z;
-    const float* dS = smem + h * (DH * DH + DH);
+  if ((int)threadIdx.x >= ch.z) return;
+  {
+    const long m = ch.y + threadIdx.x;
+    const float* dS = smem;
     const float* dz = dS + DH * DH;
     float k[DH], v[DH];
 #pragma unroll
@@ -235,24 +240,24 @@ static void allow_lds(K kernel, size_t bytes) {
 
 hipError_t launch_attn_apply_fwd(const AttnApplyArgs& a, hipStream_t s) {
   if (a.nchunks <= 0) return hipSuccess;
-  const size_t lds = (size_t)a.nsrc * a.H * (a.dh * a.dh + a.dh) * sizeof(float);
+  const size_t lds = (size_t)a.nsrc * (a.dh * a.dh + a.dh) * sizeof(float);
   GNOT_DH_SWITCH(a.dh, allow_lds(attn_apply_fwd_kernel<DH>, lds);
-                 hipLaunchKernelGGL(attn_apply_fwd_kernel<DH>, dim3(a.nchunks), dim3(256), lds, s, a));
+                 hipLaunchKernelGGL(attn_apply_fwd_kernel<DH>, dim3(a.nchunks, a.H), dim3(64), lds, s, a));
   return hipGetLastError();
 }
 
 hipError_t launch_attn_apply_bwd(const AttnApplyArgs& a, hipStream_t s) {
   if (a.nchunks <= 0) return hipSuccess;
-  const size_t lds = (size_t)a.nsrc * a.H * (a.dh * a.dh + a.dh) * sizeof(float);
+  const size_t lds = (size_t)a.nsrc * (a.dh * a.dh + a.dh) * sizeof(float);
   GNOT_DH_SWITCH(a.dh, allow_lds(attn_apply_bwd_kernel<DH>, lds);
-                 hipLaunchKernelGGL(attn_apply_bwd_kernel<DH>, dim3(a.nchunks), dim3(256), lds, s, a));
+                 hipLaunchKernelGGL(attn_apply_bwd_kernel<DH>, dim3(a.nchunks, a.H), dim3(64), lds, s, a));
   return hipGetLastError();
 }
 
 hipError_t launch_attn_kv_bwd(const AttnKVBwdArgs& a, hipStream_t s) {
   if (a.nchunks <= 0) return hipSuccess;
-  const size_t lds = (size_t)a.H * (a.dh * a.dh + a.dh) * sizeof(float);
-  GNOT_DH_SWITCH(a.dh, hipLaunchKernelGGL(attn_kv_bwd_kernel<DH>, dim3(a.nchunks), dim3(256), lds, s, a));
+  const size_t lds = (size_t)(a.dh * a.dh + a.dh) * sizeof(float);
+  GNOT_DH_SWITCH(a.dh, hipLaunchKernelGGL(attn_kv_bwd_kernel<DH>, dim3(a.nchunks, a.H), dim3(64), lds, s, a));
   return hipGetLastError();
 }
 

@@ -38,7 +38,7 @@ static int fail(int code, const std::string& msg) {
 static inline long r4(long x) { return (x + 3) & ~3L; }
 static inline int tiles16(int x) { return (x + 15) / 16; }
 
-constexpr int kSeg = 256;            // points per attention segment (state slab / apply block)
+constexpr int kSeg = 64;             // points per attention segment (one wave of the apply kernels)
 constexpr int kPTile = 128;          // output tile edge of the point-reduction GEMM (wgrad.hip)
 constexpr int kTargetWGs = 512;      // aim for ~2 workgroups per CU per point-reduction launch
 constexpr int kMinSplitPoints = 128; // never split below this many points
@@ -128,7 +128,14 @@ struct gnot_plan {
   std::vector<std::vector<WgradGroup>> st_c, dst_c;   // [l][source i]
   std::vector<WgradGroup> st_s, dst_s;                 // [l]
   size_t table_bytes = 0;
-  size_t slab_wgrad_floats = 0;
+  size_t slab_wgrad_floats = 0, slab_state_floats = 0;
+
+  // backward overlap: weight-gradient GEMMs run on a side stream; every buffer they read is
+  // double-buffered and guarded by the event of its last side-stream reader
+  hipStream_t side = nullptr;
+  std::vector<hipEvent_t> evs;
+  size_t ev_next = 0;
+  std::map<const float*, hipEvent_t> readers;
   int4* d_qchunks = nullptr;
   int* d_qchunk_off = nullptr;
   std::vector<int4*> d_fchunks;
@@ -173,6 +180,17 @@ struct gnot_plan {
   std::string block_query(int l) const {   // query entering block l
     return l == 0 ? std::string("query0") : "b" + std::to_string(l - 1) + ".query2";
   }
+  // double-buffer slots, fixed by the (static) backward order
+  std::string dz_buf(int chain_call) const { return "dz" + std::to_string(chain_call & 1); }
+  int k_out() const { return 0; }
+  int k_m2(int l) const { return 1 + 2 * (L - 1 - l); }
+  int k_m1(int l) const { return 2 + 2 * (L - 1 - l); }
+  int k_fn(int i) const { return 1 + 2 * L + i; }
+  int k_x() const { return 1 + 2 * L + I; }
+  int k_gate() const { return 2 + 2 * L + I; }
+  std::string dsum_buf(bool m1) const { return m1 ? "dsum1" : "dsum0"; }
+  std::string dqkv_buf(bool cross) const { return cross ? "dqkv1" : "dqkv0"; }
+  std::string dkv_buf(int l, int i) const { return "dkv" + std::to_string(i) + "_" + std::to_string((L - 1 - l) & 1); }
   float* P_(const char* name) const { return bufs.at(name).p; }
   float* P_(const std::string& name) const { return bufs.at(name).p; }
 };
@@ -235,6 +253,8 @@ extern "C" int gnot_plan_create(const gnot_config* cfg, gnot_plan** out) {
 extern "C" void gnot_plan_destroy(gnot_plan* plan) {
   if (!plan) return;
   for (hipEvent_t e : plan->prof_events) (void)hipEventDestroy(e);
+  for (hipEvent_t e : plan->evs) (void)hipEventDestroy(e);
+  if (plan->side) (void)hipStreamDestroy(plan->side);
   delete plan;
 }
 
@@ -437,7 +457,8 @@ static void finish_group(gnot_plan* p, WgradGroup& G) {
   }
   G.total_wgs = wg;
   G.total_red = red;
-  p->slab_wgrad_floats = std::max(p->slab_wgrad_floats, G.slab_floats);
+  size_t& slab = (!G.jobs.empty() && G.jobs[0].state_dh > 0) ? p->slab_state_floats : p->slab_wgrad_floats;
+  slab = std::max(slab, G.slab_floats);
 }
 
 template <typename F>
@@ -460,6 +481,7 @@ static void for_each_group(gnot_plan* p, F&& f) {
 // (Re)build every job list from the current buffer pointers (null before bind: sizing only).
 static void build_groups(gnot_plan* p) {
   p->slab_wgrad_floats = 0;
+  p->slab_state_floats = 0;
   const long P = p->P;
   const int D = p->D, NL = p->NL, E = p->E, I = p->I, KI = p->KI, dh = p->dh;
   const bool tr = p->training;
@@ -485,9 +507,9 @@ static void build_groups(gnot_plan* p) {
   };
   // chain c of a group: Linear j reads dZ_j from dz[(c*NL + j)*rows*D] and its input from the
   // chain input (j = 0) or gelu(saved pre-activation j-1)
-  auto chain_group = [&](WgradGroup& G, const std::vector<int>& firsts, long rows, const float* x0, long ldx0,
-                         const float* save) {
-    const float* dz = p->P_("dz");
+  auto chain_group = [&](WgradGroup& G, int kcall, const std::vector<int>& firsts, long rows, const float* x0,
+                         long ldx0, const float* save) {
+    const float* dz = p->P_(p->dz_buf(kcall));
     for (size_t c = 0; c < firsts.size(); ++c)
       for (int j = 0; j < NL; ++j) {
         const float* dzp = dz + ((long)c * NL + j) * rows * D;
@@ -543,23 +565,23 @@ static void build_groups(gnot_plan* p) {
   }
   if (!tr) return;
 
-  chain_group(p->wg_out, {p->lin_out(0)}, P, p->P_(p->final_query()), D, p->P_("out_save"));
-  chain_group(p->wg_x, {p->lin_x(0)}, P, p->P_("xin"), p->bufs.at("xin").ld, p->P_("x_save"));
-  chain_group(p->wg_gate, {p->lin_g(0)}, P, p->P_("x"), p->bufs.at("x").ld, p->P_("gate_save"));
+  chain_group(p->wg_out, p->k_out(), {p->lin_out(0)}, P, p->P_(p->final_query()), D, p->P_("out_save"));
+  chain_group(p->wg_x, p->k_x(), {p->lin_x(0)}, P, p->P_("xin"), p->bufs.at("xin").ld, p->P_("x_save"));
+  chain_group(p->wg_gate, p->k_gate(), {p->lin_g(0)}, P, p->P_("x"), p->bufs.at("x").ld, p->P_("gate_save"));
   for (int i = 0; i < I; ++i) {
     const std::string si = std::to_string(i);
-    chain_group(p->wg_fn[i], {p->lin_fn(i, 0)}, p->Q[i], p->P_("fn" + si), p->bufs.at("fn" + si).ld,
+    chain_group(p->wg_fn[i], p->k_fn(i), {p->lin_fn(i, 0)}, p->Q[i], p->P_("fn" + si), p->bufs.at("fn" + si).ld,
                 p->P_("fn_save" + si));
   }
-  float* dsum = p->P_("dsum");
-  float* dqkv = p->P_("dqkv");
   for (int l = 0; l < p->L; ++l) {
     const std::string s = "b" + std::to_string(l) + ".";
     std::vector<int> f1, f2;
     for (int e = 0; e < E; ++e) { f1.push_back(p->lin_f1(l, e, 0)); f2.push_back(p->lin_f2(l, e, 0)); }
-    chain_group(p->wg_m1[l], f1, P, p->P_(s + "a"), D, p->P_(s + "m1save"));
-    chain_group(p->wg_m2[l], f2, P, p->P_(s + "bb"), D, p->P_(s + "m2save"));
+    chain_group(p->wg_m1[l], p->k_m1(l), f1, P, p->P_(s + "a"), D, p->P_(s + "m1save"));
+    chain_group(p->wg_m2[l], p->k_m2(l), f2, P, p->P_(s + "bb"), D, p->P_(s + "m2save"));
     {
+      float* dsum = p->P_(p->dsum_buf(false));
+      float* dqkv = p->P_(p->dqkv_buf(false));
       WgradGroup& G = p->wg_self[l];
       const float* q1 = p->P_(s + "query1");
       lin_job(G, p->lin_so(l), dsum, D, p->P_(s + "sres"), D, 0, P);
@@ -569,6 +591,8 @@ static void build_groups(gnot_plan* p) {
       finish_group(p, G);
     }
     {
+      float* dsum = p->P_(p->dsum_buf(true));
+      float* dqkv = p->P_(p->dqkv_buf(true));
       WgradGroup& G = p->wg_cross[l];
       const float* qin = p->P_(p->block_query(l));
       lin_job(G, p->lin_co(l), dsum, D, p->P_(s + "cres"), D, 0, P);
@@ -576,7 +600,7 @@ static void build_groups(gnot_plan* p) {
         lin_job(G, p->lin_cq(l), dqkv, D, qin, D, 0, P);
         for (int i = 0; i < I; ++i) {
           const std::string si = std::to_string(i);
-          float* dkv = p->P_("dkv" + si);
+          float* dkv = p->P_(p->dkv_buf(l, i));
           lin_job(G, p->lin_ck(l, i), dkv, 2 * D, p->P_("fnenc" + si), D, 0, p->Q[i]);
           lin_job(G, p->lin_cv(l, i), dkv + D, 2 * D, p->P_("fnenc" + si), D, 0, p->Q[i]);
         }
@@ -683,19 +707,23 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
   if (tr) {
     C.add("dout", P * r4(p->out), r4(p->out));
     C.add("dquery", P * D, D);
-    C.add("dsum", P * D, D);
+    C.add("dsum0", P * D, D);
+    C.add("dsum1", P * D, D);
     C.add("dres", P * D, D);
-    C.add("dqkv", P * 3 * D, 3 * D);
+    C.add("dqkv0", P * 3 * D, 3 * D);
+    C.add("dqkv1", P * 3 * D, 3 * D);
     for (int i = 0; i < KI; ++i) {
       C.add("du" + std::to_string(i), P * D, D);
       C.add("dden" + std::to_string(i), P * H, H);
       C.add("dstate" + std::to_string(i), p->B * per_state, per_state);
     }
     for (int i = 0; i < I; ++i) {
-      C.add("dkv" + std::to_string(i), p->Q[i] * 2 * D, 2 * D);
+      C.add("dkv" + std::to_string(i) + "_0", p->Q[i] * 2 * D, 2 * D);
+      C.add("dkv" + std::to_string(i) + "_1", p->Q[i] * 2 * D, 2 * D);
       C.add("dfn" + std::to_string(i), p->Q[i] * D, D);
     }
-    C.add("dz", E * NL * std::max(P, Qmax) * D, D);
+    C.add("dz0", E * NL * std::max(P, Qmax) * D, D);
+    C.add("dz1", E * NL * std::max(P, Qmax) * D, D);
   }
 
   // ---------------- device tables (host images; uploaded at bind)
@@ -747,6 +775,7 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
   };
   for_each_group(p, tbl_group);
   C.add("slab_wgrad", p->slab_wgrad_floats, 0);
+  C.add("slab_state", p->slab_state_floats, 0);
   const size_t table_off = C.raw(p->table_bytes);
   p->bufs["__tables"] = Buf{table_off, 0, nullptr};
   p->ws_need = C.top;
@@ -845,9 +874,10 @@ extern "C" int gnot_plan_bind_workspace(gnot_plan* p, void* workspace, size_t by
   }
   // point-reduction GEMM groups with real pointers
   {
-    const size_t slab_need = p->slab_wgrad_floats;
+    const size_t slab_need = p->slab_wgrad_floats, slab_state_need = p->slab_state_floats;
     build_groups(p);
-    if (p->slab_wgrad_floats != slab_need) return fail(GNOT_E_INVALID, "internal: slab size changed at bind");
+    if (p->slab_wgrad_floats != slab_need || p->slab_state_floats != slab_state_need)
+      return fail(GNOT_E_INVALID, "internal: slab size changed at bind");
     for_each_group(p, [&](WgradGroup& G) {
       G.d_jobs = static_cast<WgradJob*>(put(G.jobs.data(), G.jobs.size() * sizeof(WgradJob)));
       std::vector<int> pre(G.wg_prefix);
@@ -859,6 +889,12 @@ extern "C" int gnot_plan_bind_workspace(gnot_plan* p, void* workspace, size_t by
   }
   if (cur > p->table_bytes) return fail(GNOT_E_INVALID, "internal: table overflow");
   GNOT_CK(hipMemcpy(tp, host.data(), cur, hipMemcpyHostToDevice));
+  if (p->training && !p->side) GNOT_CK(hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
+  while (p->training && p->evs.size() < 256) {
+    hipEvent_t e;
+    GNOT_CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    p->evs.push_back(e);
+  }
   p->ws_bound = true;
   p->packed = false;
   p->fwd_done = false;
@@ -886,7 +922,8 @@ struct ProfScope {
   Ctx& c;
   bool on = false;
   size_t idx = 0;
-  ProfScope(Ctx& c_, const char* kind, double flops) : c(c_) {
+  hipStream_t st;
+  ProfScope(Ctx& c_, const char* kind, double flops, hipStream_t stream = nullptr) : c(c_), st(stream ? stream : c_.s) {
     gnot_plan* p = c.p;
     if (p->prof_kind.empty() || p->prof_kind != kind) return;
     while (p->prof_events.size() < p->prof_used + 2) {
@@ -898,10 +935,10 @@ struct ProfScope {
     p->prof_used += 2;
     p->prof_flops += flops;
     p->prof_launches += 1;
-    on = hipEventRecord(p->prof_events[idx], c.s) == hipSuccess;
+    on = hipEventRecord(p->prof_events[idx], st) == hipSuccess;
   }
   ~ProfScope() {
-    if (on) (void)hipEventRecord(c.p->prof_events[idx + 1], c.s);
+    if (on) (void)hipEventRecord(c.p->prof_events[idx + 1], st);
   }
 };
 
@@ -922,13 +959,53 @@ ChainArgs chain_args(gnot_plan* p, const ChainTable& T, long P) {
   return a;
 }
 
-int run_wgrad(Ctx& c, const WgradGroup& G) {
-  if (G.jobs.empty()) return GNOT_OK;
+double group_flops(const WgradGroup& G) {
   double fl = 0.0;
   for (const auto& J : G.jobs) fl += 2.0 * J.P * (double)J.out * J.in;
-  ProfScope ps(c, G.jobs[0].state_dh > 0 ? "state" : "wgrad", fl);
+  return fl;
+}
+
+// attention-state reductions: on the main stream (they are on the critical path)
+int run_state(Ctx& c, const WgradGroup& G) {
+  if (G.jobs.empty()) return GNOT_OK;
+  ProfScope ps(c, "state", group_flops(G));
   GNOT_CK(launch_wgrad(G.d_jobs, G.d_wg_prefix, (int)G.jobs.size(), G.total_wgs, G.d_red_prefix,
-                       G.total_red, c.p->P_("slab_wgrad"), c.s));
+                       G.total_red, c.p->P_("slab_state"), c.s));
+  return GNOT_OK;
+}
+
+hipEvent_t next_event(gnot_plan* p) {
+  hipEvent_t e = p->evs[p->ev_next];
+  p->ev_next = (p->ev_next + 1) % p->evs.size();
+  return e;
+}
+
+// before the main stream overwrites `buf`, wait for the side-stream group that last read it
+int guard_write(Ctx& c, const float* buf) {
+  auto it = c.p->readers.find(buf);
+  if (it != c.p->readers.end()) {
+    GNOT_CK(hipStreamWaitEvent(c.s, it->second, 0));
+    c.p->readers.erase(it);
+  }
+  return GNOT_OK;
+}
+
+// weight gradients: forked onto the side stream (off the critical path); `reads` are the main-stream
+// buffers the group consumes, guarded until it finishes
+int run_wgrad_side(Ctx& c, const WgradGroup& G, std::initializer_list<const float*> reads) {
+  if (G.jobs.empty()) return GNOT_OK;
+  gnot_plan* p = c.p;
+  hipEvent_t fork = next_event(p);
+  GNOT_CK(hipEventRecord(fork, c.s));
+  GNOT_CK(hipStreamWaitEvent(p->side, fork, 0));
+  {
+    ProfScope ps(c, "wgrad", group_flops(G), p->side);
+    GNOT_CK(launch_wgrad(G.d_jobs, G.d_wg_prefix, (int)G.jobs.size(), G.total_wgs, G.d_red_prefix,
+                         G.total_red, p->P_("slab_wgrad"), p->side));
+  }
+  hipEvent_t done = next_event(p);
+  GNOT_CK(hipEventRecord(done, p->side));
+  for (const float* r : reads) p->readers[r] = done;
   return GNOT_OK;
 }
 
@@ -956,7 +1033,7 @@ int attn_forward(Ctx& c, int l, bool cross, const float* q_in, float* res_out, f
       float* kv = p->P_(s + "ckv" + si);
       GNOT_RUN(run_linear(c, p->P_("fnenc" + si), D, D, A.kv[i], pbias + A.bkv[i], kv, 2 * D, 2 * D, p->Q[i],
                           EPI_STORE, D));
-      GNOT_RUN(run_wgrad(c, p->st_c[l][i]));
+      GNOT_RUN(run_state(c, p->st_c[l][i]));
       ap.state[i] = p->P_(s + "cstate" + si);
     }
     ap.q = q; ap.ldq = D; ap.nsrc = p->I; ap.chunks = p->d_qchunks; ap.nchunks = nq; ap.off = p->d_xoff;
@@ -966,7 +1043,7 @@ int attn_forward(Ctx& c, int l, bool cross, const float* q_in, float* res_out, f
     float* qkv = p->P_(cross ? s + "cq" : s + "sq");
     GNOT_RUN(run_linear(c, q_in, D, D, A.qkv, pbias + A.bqkv, qkv, 3 * D, 3 * D, P, EPI_STORE, 2 * D));
     float* st = p->P_(cross ? s + "cstate0" : s + "sstate");
-    GNOT_RUN(run_wgrad(c, cross ? p->st_c[l][0] : p->st_s[l]));
+    GNOT_RUN(run_state(c, cross ? p->st_c[l][0] : p->st_s[l]));
     AttnApplyArgs ap{};
     ap.q = qkv; ap.ldq = 3 * D; ap.nsrc = 1; ap.state[0] = st; ap.chunks = p->d_qchunks; ap.nchunks = nq;
     ap.off = p->d_xoff; ap.H = p->H; ap.dh = p->dh; ap.res = res_out;
@@ -976,20 +1053,21 @@ int attn_forward(Ctx& c, int l, bool cross, const float* q_in, float* res_out, f
   return GNOT_OK;
 }
 
-// backward of one LinearAttention call. dout: grad of its output [P, D] (materialised in "dsum").
-// Accumulates d(q_in) into dquery.
-int attn_backward(Ctx& c, int l, bool cross, const float* q_in) {
+// backward of one LinearAttention call; its output gradient is materialised in dsum_buf(cross).
+// Accumulates d(query input) into dquery and forks the weight gradients of its 4+ Linears.
+int attn_backward(Ctx& c, int l, bool cross) {
   gnot_plan* p = c.p;
   const long P = p->P;
   const int D = p->D;
   const std::string s = "b" + std::to_string(l) + ".";
   const int lo = cross ? p->lin_co(l) : p->lin_so(l);
   const int lq = cross ? p->lin_cq(l) : p->lin_sq(l);
-  float* dsum = p->P_("dsum");
+  float* dsum = p->P_(p->dsum_buf(cross));
   float* dres = p->P_("dres");
   float* dquery = p->P_("dquery");
-  float* dqkv = p->P_("dqkv");
+  float* dqkv = p->P_(p->dqkv_buf(cross));
   const int nq = (int)p->qchunks.size();
+  GNOT_RUN(guard_write(c, dqkv));
   // fc_out backward-data: dres = dout W_o
   GNOT_RUN(run_linear(c, dsum, D, D, p->T_img[lo], nullptr, dres, D, D, P, EPI_STORE, 0));
   if (cross && p->I > 0) {
@@ -1004,12 +1082,14 @@ int attn_backward(Ctx& c, int l, bool cross, const float* q_in) {
       ap.dden[i] = p->P_("dden" + si);
     }
     GNOT_CK(launch_attn_apply_bwd(ap, c.s));
+    std::vector<const float*> dkvs;
     for (int i = 0; i < p->I; ++i) {
       const std::string si = std::to_string(i);
       float* dst = p->P_("dstate" + si);
-      GNOT_RUN(run_wgrad(c, p->dst_c[l][i]));
+      GNOT_RUN(run_state(c, p->dst_c[l][i]));
       const float* kv = p->P_(s + "ckv" + si);
-      float* dkv = p->P_("dkv" + si);
+      float* dkv = p->P_(p->dkv_buf(l, i));
+      GNOT_RUN(guard_write(c, dkv));
       AttnKVBwdArgs kb{};
       kb.k = kv; kb.v = kv + D; kb.ldkv = 2 * D; kb.dstate = dst; kb.chunks = p->d_fchunks[i];
       kb.nchunks = (int)p->fchunks[i].size(); kb.H = p->H; kb.dh = p->dh; kb.dk = dkv; kb.dv = dkv + D;
@@ -1018,8 +1098,11 @@ int attn_backward(Ctx& c, int l, bool cross, const float* q_in) {
       float* dfn = p->P_("dfn" + si);
       GNOT_RUN(run_linear(c, dkv, 2 * D, D, p->T_img[p->lin_ck(l, i)], nullptr, dfn, D, D, p->Q[i], EPI_ACCUM, 0));
       GNOT_RUN(run_linear(c, dkv + D, 2 * D, D, p->T_img[p->lin_cv(l, i)], nullptr, dfn, D, D, p->Q[i], EPI_ACCUM, 0));
+      dkvs.push_back(dkv);
     }
     GNOT_RUN(run_linear(c, dqkv, D, D, p->T_img[lq], nullptr, dquery, D, D, P, EPI_ACCUM, 0));
+    GNOT_RUN(run_wgrad_side(c, p->wg_cross[l], {dsum, dqkv}));
+    for (const float* d : dkvs) p->readers[d] = p->readers[dsum];
   } else {
     const float* qkv = p->P_(cross ? s + "cq" : s + "sq");
     const int lk = cross ? p->lin_ck(l, 0) : p->lin_sk(l);
@@ -1031,7 +1114,7 @@ int attn_backward(Ctx& c, int l, bool cross, const float* q_in) {
     ap.dden[0] = p->P_("dden0");
     GNOT_CK(launch_attn_apply_bwd(ap, c.s));
     float* dst = p->P_("dstate0");
-    GNOT_RUN(run_wgrad(c, cross ? p->dst_c[l][0] : p->dst_s[l]));
+    GNOT_RUN(run_state(c, cross ? p->dst_c[l][0] : p->dst_s[l]));
     AttnKVBwdArgs kb{};
     kb.k = qkv + D; kb.v = qkv + 2 * D; kb.ldkv = 3 * D; kb.dstate = dst; kb.chunks = p->d_qchunks;
     kb.nchunks = nq; kb.H = p->H; kb.dh = p->dh; kb.dk = dqkv + D; kb.dv = dqkv + 2 * D; kb.lddkv = 3 * D;
@@ -1039,8 +1122,8 @@ int attn_backward(Ctx& c, int l, bool cross, const float* q_in) {
     GNOT_RUN(run_linear(c, dqkv, 3 * D, D, p->T_img[lq], nullptr, dquery, D, D, P, EPI_ACCUM, 0));
     GNOT_RUN(run_linear(c, dqkv + D, 3 * D, D, p->T_img[lk], nullptr, dquery, D, D, P, EPI_ACCUM, 0));
     GNOT_RUN(run_linear(c, dqkv + 2 * D, 3 * D, D, p->T_img[lv], nullptr, dquery, D, D, P, EPI_ACCUM, 0));
+    GNOT_RUN(run_wgrad_side(c, cross ? p->wg_cross[l] : p->wg_self[l], {dsum, dqkv}));
   }
-  (void)q_in;
   return GNOT_OK;
 }
 
@@ -1138,60 +1221,51 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
   Ctx c{p, static_cast<hipStream_t>(stream)};
   const long P = p->P;
   const int D = p->D, E = p->E, NL = p->NL;
-  float* dz = p->P_("dz");
   float* dquery = p->P_("dquery");
   float* stage = p->P_("stage");
+  p->readers.clear();
   GNOT_CK(hipMemcpy2DAsync(p->P_("dout"), p->bufs["dout"].ld * 4, dout, p->out * 4, p->out * 4, P,
                            hipMemcpyDeviceToDevice, c.s));
   GNOT_CK(hipMemsetAsync(p->P_("dscore"), 0, P * p->bufs["dscore"].ld * 4, c.s));
   for (int i = 0; i < p->I; ++i)
     GNOT_CK(hipMemsetAsync(p->P_("dfn" + std::to_string(i)), 0, p->Q[i] * D * 4, c.s));
-  // decoder
+  // one chain backward: dZ of every Linear into the chain call's dz slot, then its weight gradients
+  // are forked to the side stream
+  auto chain_bwd = [&](ChainArgs& a, int kcall, long rows, const WgradGroup& G, const char* prof) -> int {
+    float* dz = p->P_(p->dz_buf(kcall));
+    GNOT_RUN(guard_write(c, dz));
+    a.dz = dz; a.dz_layer_stride = rows * D; a.dz_chain_stride = NL * rows * D;
+    {
+      ProfScope ps(c, prof, 2.0 * a.nchains * rows * NL * (double)D * D);
+      GNOT_CK(launch_chain_bwd(a, c.s));
+    }
+    return run_wgrad_side(c, G, {dz});
+  };
+  // decoder (model.py:171)
   {
     ChainArgs a = chain_args(p, p->ch_out, P);
     a.dY = p->P_("dout"); a.lddy = p->bufs["dout"].ld; a.mode = CH_STORE;
     a.save = p->P_("out_save"); a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D;
-    a.dz = dz; a.dz_layer_stride = P * D; a.dz_chain_stride = NL * P * D;
     a.dX = dquery; a.lddx = D; a.dx_chain_stride = 0;
-    GNOT_CK(launch_chain_bwd(a, c.s));
-    GNOT_RUN(run_wgrad(c, p->wg_out));
+    GNOT_RUN(chain_bwd(a, p->k_out(), P, p->wg_out, "chain_bwd"));
   }
   for (int l = p->L - 1; l >= 0; --l) {
     const std::string s = "b" + std::to_string(l) + ".";
-    // ffn2 experts: query2 = query1 + sum_e s_e ffn2_e(bb)
-    {
-      ChainArgs a = chain_args(p, p->ch_m2[l], P);
+    // ffn2 experts: query2 = query1 + sum_e s_e ffn2_e(bb)   (model.py:134-137)
+    for (int m = 2; m >= 1; --m) {
+      const bool m1 = (m == 1);
+      ChainArgs a = chain_args(p, m1 ? p->ch_m1[l] : p->ch_m2[l], P);
       a.dY = dquery; a.lddy = D; a.mode = CH_MOE;
       a.scores = p->P_("scores"); a.ldsc = (int)p->bufs["scores"].ld; a.dscore = p->P_("dscore");
-      a.save = p->P_(s + "m2save"); a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D;
-      a.dz = dz; a.dz_layer_stride = P * D; a.dz_chain_stride = NL * P * D;
+      a.save = p->P_(s + (m1 ? "m1save" : "m2save")); a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D;
       a.dX = stage; a.lddx = D; a.dx_chain_stride = P * D;
-      {
-        ProfScope ps(c, "moe_bwd", 2.0 * E * P * NL * (double)D * D);
-        GNOT_CK(launch_chain_bwd(a, c.s));
-      }
-      GNOT_RUN(run_wgrad(c, p->wg_m2[l]));
-      GNOT_CK(launch_moe_combine(nullptr, stage, P * D, E, p->P_("dsum"), P * D, c.s));
+      GNOT_RUN(chain_bwd(a, m1 ? p->k_m1(l) : p->k_m2(l), P, m1 ? p->wg_m1[l] : p->wg_m2[l], "moe_bwd"));
+      float* dsum = p->P_(p->dsum_buf(m1));
+      GNOT_RUN(guard_write(c, dsum));
+      GNOT_CK(launch_moe_combine(nullptr, stage, P * D, E, dsum, P * D, c.s));
+      // m2: self attention (model.py:133) ; m1: cross attention (model.py:127)
+      GNOT_RUN(attn_backward(c, l, m1));
     }
-    GNOT_RUN(attn_backward(c, l, false, p->P_(s + "query1")));
-    GNOT_RUN(run_wgrad(c, p->wg_self[l]));
-    // ffn1 experts: query1 = query0 + sum_e s_e ffn1_e(a)
-    {
-      ChainArgs a = chain_args(p, p->ch_m1[l], P);
-      a.dY = dquery; a.lddy = D; a.mode = CH_MOE;
-      a.scores = p->P_("scores"); a.ldsc = (int)p->bufs["scores"].ld; a.dscore = p->P_("dscore");
-      a.save = p->P_(s + "m1save"); a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D;
-      a.dz = dz; a.dz_layer_stride = P * D; a.dz_chain_stride = NL * P * D;
-      a.dX = stage; a.lddx = D; a.dx_chain_stride = P * D;
-      {
-        ProfScope ps(c, "moe_bwd", 2.0 * E * P * NL * (double)D * D);
-        GNOT_CK(launch_chain_bwd(a, c.s));
-      }
-      GNOT_RUN(run_wgrad(c, p->wg_m1[l]));
-      GNOT_CK(launch_moe_combine(nullptr, stage, P * D, E, p->P_("dsum"), P * D, c.s));
-    }
-    GNOT_RUN(attn_backward(c, l, true, p->P_(p->block_query(l))));
-    GNOT_RUN(run_wgrad(c, p->wg_cross[l]));
   }
   // input-function encoders (their inputs need no gradient)
   for (int i = 0; i < p->I; ++i) {
@@ -1199,18 +1273,14 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
     ChainArgs a = chain_args(p, p->ch_fn[i], p->Q[i]);
     a.dY = p->P_("dfn" + si); a.lddy = D; a.mode = CH_STORE;
     a.save = p->P_("fn_save" + si); a.save_layer_stride = p->Q[i] * D; a.save_chain_stride = NL * p->Q[i] * D;
-    a.dz = dz; a.dz_layer_stride = p->Q[i] * D; a.dz_chain_stride = NL * p->Q[i] * D;
-    GNOT_CK(launch_chain_bwd(a, c.s));
-    GNOT_RUN(run_wgrad(c, p->wg_fn[i]));
+    GNOT_RUN(chain_bwd(a, p->k_fn(i), p->Q[i], p->wg_fn[i], "chain_bwd"));
   }
   // query encoder
   {
     ChainArgs a = chain_args(p, p->ch_x, P);
     a.dY = dquery; a.lddy = D; a.mode = CH_STORE;
     a.save = p->P_("x_save"); a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D;
-    a.dz = dz; a.dz_layer_stride = P * D; a.dz_chain_stride = NL * P * D;
-    GNOT_CK(launch_chain_bwd(a, c.s));
-    GNOT_RUN(run_wgrad(c, p->wg_x));
+    GNOT_RUN(chain_bwd(a, p->k_x(), P, p->wg_x, "chain_bwd"));
   }
   // gating: d scores accumulated over every MoE above -> softmax backward -> chain
   {
@@ -1218,11 +1288,13 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
     a.mode = CH_SOFTMAX; a.scores = p->P_("scores"); a.ldsc = (int)p->bufs["scores"].ld;
     a.dscore = p->P_("dscore");
     a.save = p->P_("gate_save"); a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D;
-    a.dz = dz; a.dz_layer_stride = P * D; a.dz_chain_stride = NL * P * D;
-    GNOT_CK(launch_chain_bwd(a, c.s));
-    GNOT_RUN(run_wgrad(c, p->wg_gate));
+    GNOT_RUN(chain_bwd(a, p->k_gate(), P, p->wg_gate, "chain_bwd"));
   }
-  (void)E;
+  // join the side stream: every gradient is complete when the caller's stream moves on
+  hipEvent_t join = next_event(p);
+  GNOT_CK(hipEventRecord(join, p->side));
+  GNOT_CK(hipStreamWaitEvent(c.s, join, 0));
+  p->readers.clear();
   return GNOT_OK;
 }
 
