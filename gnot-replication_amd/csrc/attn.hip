@@ -10,8 +10,8 @@
 // at flat offset off_b*d + (h*N_b + n)*dh + j, and fc_out reads that buffer as plain rows.
 //
 // Kernels here:
-//   attn_apply_fwd / attn_apply_bwd  grid (64-point segment, head): one wave, one thread per point,
-//                the head's (S, z) of every source staged in LDS and read as broadcasts.
+//   attn_apply_fwd / attn_apply_bwd  one 64-point segment per workgroup, one thread per (point, head)
+//                in point-major order (coalesced row reads); every head's (S, z) staged in LDS.
 //   attn_kv_bwd  dK, dV from (dS, dz) per (source point, head), same geometry.
 // The cross-point reductions themselves (S, z forward; dS, dz backward) are point-reduction GEMMs
 // on the MFMA path (wgrad.hip, state jobs), one job per sample.
@@ -55,26 +55,26 @@ GNOT_DEV float dot_row(const float (&x)[DH], const float* row) {
 
 // ---------------------------------------------------------------- apply (forward)
 template <int DH>
-__global__ void __launch_bounds__(64) attn_apply_fwd_kernel(AttnApplyArgs a) {
+__global__ void __launch_bounds__(256) attn_apply_fwd_kernel(AttnApplyArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int4 ch = a.chunks[blockIdx.x];
   const int b = ch.x;
   const int H = a.H;
-  const int h = blockIdx.y;                 // one wave = up to 64 points of ONE head: LDS broadcasts
   constexpr int ph = DH * DH + DH;
   const int per = H * ph;
-  for (int i = threadIdx.x; i < a.nsrc * ph; i += 64) {
-    const int sidx = i / ph, e = i % ph;
-    smem[i] = a.state[sidx][(long)b * per + h * ph + e];
+  for (int i = threadIdx.x; i < a.nsrc * per; i += 256) {
+    const int sidx = i / per, e = i % per;
+    smem[i] = a.state[sidx][(long)b * per + e];
   }
   __syncthreads();
-  if ((int)threadIdx.x >= ch.z) return;
   const long off_b = a.off[b];
   const long Nb = a.off[b + 1] - off_b;
   const int d = H * DH;
   const float inv_nsrc = 1.0f / (float)a.nsrc;
-  {
-    const long n = ch.y + threadIdx.x;  // global point index
+  // point-major work order: consecutive lanes read consecutive heads of one point row (coalesced)
+  for (int idx = threadIdx.x; idx < ch.z * H; idx += 256) {
+    const long n = ch.y + idx / H;       // global point index
+    const int h = idx % H;
     float q[DH], os[DH];
 #pragma unroll
     for (int j = 0; j < DH; j += 4) {
@@ -84,7 +84,7 @@ __global__ void __launch_bounds__(64) attn_apply_fwd_kernel(AttnApplyArgs a) {
 #pragma unroll
     for (int j = 0; j < DH; ++j) os[j] = 0.f;
     for (int sidx = 0; sidx < a.nsrc; ++sidx) {
-      const float* S = smem + sidx * ph;
+      const float* S = smem + sidx * per + h * ph;
       const float* z = S + DH * DH;
       float den = 0.f;
 #pragma unroll
@@ -106,26 +106,25 @@ __global__ void __launch_bounds__(64) attn_apply_fwd_kernel(AttnApplyArgs a) {
 
 // ---------------------------------------------------------------- apply (backward)
 template <int DH>
-__global__ void __launch_bounds__(64) attn_apply_bwd_kernel(AttnApplyArgs a) {
+__global__ void __launch_bounds__(256) attn_apply_bwd_kernel(AttnApplyArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int4 ch = a.chunks[blockIdx.x];
   const int b = ch.x;
   const int H = a.H;
-  const int h = blockIdx.y;
   constexpr int ph = DH * DH + DH;
   const int per = H * ph;
-  for (int i = threadIdx.x; i < a.nsrc * ph; i += 64) {
-    const int sidx = i / ph, e = i % ph;
-    smem[i] = a.state[sidx][(long)b * per + h * ph + e];
+  for (int i = threadIdx.x; i < a.nsrc * per; i += 256) {
+    const int sidx = i / per, e = i % per;
+    smem[i] = a.state[sidx][(long)b * per + e];
   }
   __syncthreads();
-  if ((int)threadIdx.x >= ch.z) return;
   const long off_b = a.off[b];
   const long Nb = a.off[b + 1] - off_b;
   const int d = H * DH;
   const float inv_nsrc = 1.0f / (float)a.nsrc;
-  {
-    const long n = ch.y + threadIdx.x;
+  for (int idx = threadIdx.x; idx < ch.z * H; idx += 256) {
+    const long n = ch.y + idx / H;
+    const int h = idx % H;
     float q[DH], dO[DH], dq[DH];
     const float* src = a.dres + off_b * d + ((long)h * Nb + (n - off_b)) * DH;
 #pragma unroll
@@ -138,7 +137,7 @@ __global__ void __launch_bounds__(64) attn_apply_bwd_kernel(AttnApplyArgs a) {
 #pragma unroll
     for (int j = 0; j < DH; ++j) dO[j] = dq[j] * inv_nsrc;
     for (int sidx = 0; sidx < a.nsrc; ++sidx) {
-      const float* S = smem + sidx * ph;
+      const float* S = smem + sidx * per + h * ph;
       const float* z = S + DH * DH;
       float den = 0.f;
 #pragma unroll
@@ -178,20 +177,19 @@ __global__ void __launch_bounds__(64) attn_apply_bwd_kernel(AttnApplyArgs a) {
 
 // ---------------------------------------------------------------- K/V backward
 template <int DH>
-__global__ void __launch_bounds__(64) attn_kv_bwd_kernel(AttnKVBwdArgs a) {
+__global__ void __launch_bounds__(256) attn_kv_bwd_kernel(AttnKVBwdArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int4 ch = a.chunks[blockIdx.x];
   const int b = ch.x;
   const int H = a.H;
-  const int h = blockIdx.y;
   constexpr int ph = DH * DH + DH;
   const int per = H * ph;
-  for (int i = threadIdx.x; i < ph; i += 64) smem[i] = a.dstate[(long)b * per + h * ph + i];
+  for (int i = threadIdx.x; i < per; i += 256) smem[i] = a.dstate[(long)b * per + i];
   __syncthreads();
-  if ((int)threadIdx.x >= ch.z) return;
-  {
-    const long m = ch.y + threadIdx.x;
-    const float* dS = smem;
+  for (int idx = threadIdx.x; idx < ch.z * H; idx += 256) {
+    const long m = ch.y + idx / H;
+    const int h = idx % H;
+    const float* dS = smem + h * ph;
     const float* dz = dS + DH * DH;
     float k[DH], v[DH];
 #pragma unroll
@@ -240,24 +238,25 @@ static void allow_lds(K kernel, size_t bytes) {
 
 hipError_t launch_attn_apply_fwd(const AttnApplyArgs& a, hipStream_t s) {
   if (a.nchunks <= 0) return hipSuccess;
-  const size_t lds = (size_t)a.nsrc * (a.dh * a.dh + a.dh) * sizeof(float);
+  const size_t lds = (size_t)a.nsrc * a.H * (a.dh * a.dh + a.dh) * sizeof(float);
   GNOT_DH_SWITCH(a.dh, allow_lds(attn_apply_fwd_kernel<DH>, lds);
-                 hipLaunchKernelGGL(attn_apply_fwd_kernel<DH>, dim3(a.nchunks, a.H), dim3(64), lds, s, a));
+                 hipLaunchKernelGGL(attn_apply_fwd_kernel<DH>, dim3(a.nchunks), dim3(256), lds, s, a));
   return hipGetLastError();
 }
 
 hipError_t launch_attn_apply_bwd(const AttnApplyArgs& a, hipStream_t s) {
   if (a.nchunks <= 0) return hipSuccess;
-  const size_t lds = (size_t)a.nsrc * (a.dh * a.dh + a.dh) * sizeof(float);
+  const size_t lds = (size_t)a.nsrc * a.H * (a.dh * a.dh + a.dh) * sizeof(float);
   GNOT_DH_SWITCH(a.dh, allow_lds(attn_apply_bwd_kernel<DH>, lds);
-                 hipLaunchKernelGGL(attn_apply_bwd_kernel<DH>, dim3(a.nchunks, a.H), dim3(64), lds, s, a));
+                 hipLaunchKernelGGL(attn_apply_bwd_kernel<DH>, dim3(a.nchunks), dim3(256), lds, s, a));
   return hipGetLastError();
 }
 
 hipError_t launch_attn_kv_bwd(const AttnKVBwdArgs& a, hipStream_t s) {
   if (a.nchunks <= 0) return hipSuccess;
-  const size_t lds = (size_t)(a.dh * a.dh + a.dh) * sizeof(float);
-  GNOT_DH_SWITCH(a.dh, hipLaunchKernelGGL(attn_kv_bwd_kernel<DH>, dim3(a.nchunks, a.H), dim3(64), lds, s, a));
+  const size_t lds = (size_t)a.H * (a.dh * a.dh + a.dh) * sizeof(float);
+  GNOT_DH_SWITCH(a.dh, allow_lds(attn_kv_bwd_kernel<DH>, lds);
+                 hipLaunchKernelGGL(attn_kv_bwd_kernel<DH>, dim3(a.nchunks), dim3(256), lds, s, a));
   return hipGetLastError();
 }
 

@@ -17,10 +17,6 @@
 
 namespace gnot {
 
-// LDS capacity (float4) for the largest layer chunk of a width-D chain
-template <int D>
-constexpr int kLdsF4 = (D / 16) * lds_och(D / 16, D / 16) * WAVE;
-
 template <int D, int KT0, int OTL>
 __global__ void __launch_bounds__(256) chain_fwd_kernel(ChainArgs a) {
   constexpr int DT = D / 16;
@@ -29,9 +25,14 @@ __global__ void __launch_bounds__(256) chain_fwd_kernel(ChainArgs a) {
   const long p = ((long)blockIdx.x * 4 + wave) * 16 + (lane & 15);
   const bool valid = p < a.P;
   const int e = blockIdx.y;
-  const ChainLayer* L = a.layers + e * a.nlin;
+  const int nl = a.nlin;
+  const ChainLayer* L = a.layers + e * nl;
   float* save = a.save ? a.save + e * a.save_chain_stride : nullptr;
-  __shared__ __attribute__((aligned(16))) float4 wlds[kLdsF4<D>];
+  __shared__ __attribute__((aligned(16))) float4 wlds[2 * kChunkF4];
+  int cnt = 0;
+  // the weight stream: layer 0 | hidden layers | last layer, one chunk always in flight
+  stage_image(wlds, L[0].Wp, chunk_f4(KT0, DT), 4, wave, lane);
+  auto next_f4 = [&](int l) { return (l == nl - 1) ? chunk_f4(DT, OTL) : chunk_f4(DT, DT); };
 
   float h[DT][4];
   {
@@ -39,7 +40,7 @@ __global__ void __launch_bounds__(256) chain_fwd_kernel(ChainArgs a) {
     load_rows<KT0>(x0, a.X, a.ldx, p, valid, a.in_dim, lane);
     f32x4 acc[DT];
     init_bias<DT>(acc, L[0].bias, lane);
-    mm_tiles_lds<KT0, DT>(L[0].Wp, wlds, x0, acc, 4, wave, lane);
+    mm_tiles_pipe<KT0, DT>(L[0].Wp, L[1].Wp, next_f4(1), wlds, cnt, x0, acc, 4, wave, lane);
     acc_to_regs<DT>(acc, h);
   }
   if (save) store_rows<DT>(h, save, D, p, valid, D, lane);
@@ -48,10 +49,10 @@ __global__ void __launch_bounds__(256) chain_fwd_kernel(ChainArgs a) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) h[T][r] = gelu(h[T][r]);
 
-  for (int l = 1; l < a.nlin - 1; ++l) {
+  for (int l = 1; l < nl - 1; ++l) {
     f32x4 acc[DT];
     init_bias<DT>(acc, L[l].bias, lane);
-    mm_tiles_lds<DT, DT>(L[l].Wp, wlds, h, acc, 4, wave, lane);
+    mm_tiles_pipe<DT, DT>(L[l].Wp, L[l + 1].Wp, next_f4(l + 1), wlds, cnt, h, acc, 4, wave, lane);
     acc_to_regs<DT>(acc, h);
     if (save) store_rows<DT>(h, save + l * a.save_layer_stride, D, p, valid, D, lane);
 #pragma unroll
@@ -63,11 +64,11 @@ __global__ void __launch_bounds__(256) chain_fwd_kernel(ChainArgs a) {
   float y[OTL][4];
   {
     f32x4 acc[OTL];
-    init_bias<OTL>(acc, L[a.nlin - 1].bias, lane);
-    mm_tiles_lds<DT, OTL>(L[a.nlin - 1].Wp, wlds, h, acc, 4, wave, lane);
+    init_bias<OTL>(acc, L[nl - 1].bias, lane);
+    mm_tiles_pipe<DT, OTL>(L[nl - 1].Wp, nullptr, 0, wlds, cnt, h, acc, 4, wave, lane);
     acc_to_regs<OTL>(acc, y);
   }
-  if (save) store_rows<OTL>(y, save + (a.nlin - 1) * a.save_layer_stride, D, p, valid, 16 * OTL, lane);
+  if (save) store_rows<OTL>(y, save + (nl - 1) * a.save_layer_stride, D, p, valid, 16 * OTL, lane);
 
   const int g = lane >> 4;
   if (a.mode == CH_SOFTMAX) {
@@ -118,10 +119,19 @@ __global__ void __launch_bounds__(256) chain_bwd_kernel(ChainArgs a) {
   const long p = ((long)blockIdx.x * 4 + wave) * 16 + (lane & 15);
   const bool valid = p < a.P;
   const int e = blockIdx.y;
-  const ChainLayer* L = a.layers + e * a.nlin;
+  const int nl = a.nlin;
+  const ChainLayer* L = a.layers + e * nl;
   const float* save = a.save + e * a.save_chain_stride;
-  __shared__ __attribute__((aligned(16))) float4 wlds[kLdsF4<D>];
   float* dz = a.dz ? a.dz + e * a.dz_chain_stride : nullptr;
+  __shared__ __attribute__((aligned(16))) float4 wlds[2 * kChunkF4];
+  int cnt = 0;
+  // transposed-weight stream in reverse layer order: last | hidden (nl-2 .. 1) | first (if dX)
+  stage_image(wlds, L[nl - 1].WpT, chunk_f4(OTL, DT), 4, wave, lane);
+  auto next_W = [&](int l) -> const float4* {      // the layer processed after layer l
+    if (l - 1 >= 1) return L[l - 1].WpT;
+    return a.dX ? L[0].WpT : nullptr;
+  };
+  auto next_f4 = [&](int l) { return (l - 1 >= 1) ? chunk_f4(DT, DT) : chunk_f4(DT, KT0); };
 
   // ---- gradient at the chain output
   float dy[OTL][4];
@@ -129,7 +139,7 @@ __global__ void __launch_bounds__(256) chain_bwd_kernel(ChainArgs a) {
     // query_out = query_in + sum_e s_e * y_e : dy_e = s_e * dq ; ds_e = dq . y_e (model.py:128-131)
     float yv[OTL][4];
     load_rows<OTL>(dy, a.dY, a.lddy, p, valid, 16 * OTL, lane);
-    load_rows<OTL>(yv, save + (a.nlin - 1) * a.save_layer_stride, D, p, valid, 16 * OTL, lane);
+    load_rows<OTL>(yv, save + (nl - 1) * a.save_layer_stride, D, p, valid, 16 * OTL, lane);
     float ds = 0.f;
 #pragma unroll
     for (int T = 0; T < OTL; ++T)
@@ -163,19 +173,20 @@ __global__ void __launch_bounds__(256) chain_bwd_kernel(ChainArgs a) {
     load_rows<OTL>(dy, a.dY, a.lddy, p, valid, a.out_dim, lane);
   }
 
-  // ---- last Linear
-  if (dz) store_rows<OTL>(dy, dz + (a.nlin - 1) * a.dz_layer_stride, D, p, valid, 16 * OTL, lane);
+  // ---- last Linear; the saved pre-activation of Linear nl-2 is prefetched during its MFMAs
+  if (dz) store_rows<OTL>(dy, dz + (nl - 1) * a.dz_layer_stride, D, p, valid, 16 * OTL, lane);
   float gr[DT][4];
+  float hs[DT][4];
   {
     f32x4 acc[DT];
     init_bias<DT>(acc, nullptr, lane);
-    mm_tiles_lds<OTL, DT>(L[a.nlin - 1].WpT, wlds, dy, acc, 4, wave, lane);
+    auto pre = [&]() { load_rows<DT>(hs, save + (nl - 2) * a.save_layer_stride, D, p, valid, D, lane); };
+    mm_tiles_pipe<OTL, DT>(L[nl - 1].WpT, next_W(nl - 1), next_f4(nl - 1), wlds, cnt, dy, acc, 4, wave, lane,
+                           pre);
     acc_to_regs<DT>(acc, gr);
   }
   // ---- hidden Linears, reverse
-  for (int l = a.nlin - 2; l >= 1; --l) {
-    float hs[DT][4];
-    load_rows<DT>(hs, save + l * a.save_layer_stride, D, p, valid, D, lane);
+  for (int l = nl - 2; l >= 1; --l) {
 #pragma unroll
     for (int T = 0; T < DT; ++T)
 #pragma unroll
@@ -183,23 +194,20 @@ __global__ void __launch_bounds__(256) chain_bwd_kernel(ChainArgs a) {
     if (dz) store_rows<DT>(gr, dz + l * a.dz_layer_stride, D, p, valid, D, lane);
     f32x4 acc[DT];
     init_bias<DT>(acc, nullptr, lane);
-    mm_tiles_lds<DT, DT>(L[l].WpT, wlds, gr, acc, 4, wave, lane);
+    auto pre = [&]() { load_rows<DT>(hs, save + (l - 1) * a.save_layer_stride, D, p, valid, D, lane); };
+    mm_tiles_pipe<DT, DT>(L[l].WpT, next_W(l), next_f4(l), wlds, cnt, gr, acc, 4, wave, lane, pre);
     acc_to_regs<DT>(acc, gr);
   }
-  // ---- first Linear
-  {
-    float hs[DT][4];
-    load_rows<DT>(hs, save, D, p, valid, D, lane);
+  // ---- first Linear (hs now holds the saved pre-activation of Linear 0)
 #pragma unroll
-    for (int T = 0; T < DT; ++T)
+  for (int T = 0; T < DT; ++T)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) gr[T][r] *= gelu_grad(hs[T][r]);
-    if (dz) store_rows<DT>(gr, dz, D, p, valid, D, lane);
-  }
+    for (int r = 0; r < 4; ++r) gr[T][r] *= gelu_grad(hs[T][r]);
+  if (dz) store_rows<DT>(gr, dz, D, p, valid, D, lane);
   if (a.dX) {
     f32x4 acc[KT0];
     init_bias<KT0>(acc, nullptr, lane);
-    mm_tiles_lds<DT, KT0>(L[0].WpT, wlds, gr, acc, 4, wave, lane);
+    mm_tiles_pipe<DT, KT0>(L[0].WpT, nullptr, 0, wlds, cnt, gr, acc, 4, wave, lane);
     float dx[KT0][4];
     acc_to_regs<KT0>(acc, dx);
     store_rows<KT0>(dx, a.dX + e * a.dx_chain_stride, a.lddx, p, valid, a.in_dim, lane);

@@ -157,14 +157,92 @@ GNOT_DEV void mm_tiles_lds(const float4* __restrict__ Wg, float4* lds, const flo
     __syncthreads();                                   // previous readers of lds are done
     stage_image(lds, Wg + c * OCH * KT * WAVE, OCH * KT * WAVE, nwaves, wave, lane);
     __syncthreads();                                   // drains the LDS-DMA (vmcnt(0)) + barrier
+    // fragments of k-tile T+1 are read from LDS while the MFMAs of k-tile T run; within a k-tile the
+    // MFMA order is k-step-outer / output-tile-inner, so consecutive MFMAs use independent
+    // accumulators (the f32 16x16x4 MFMA has a 40-cycle dependent latency vs 32-cycle issue)
+    float4 wc[OCH], wn[OCH];
+#pragma unroll
+    for (int o = 0; o < OCH; ++o) wc[o] = lds[(o * KT + 0) * WAVE + lane];
 #pragma unroll
     for (int T = 0; T < KT; ++T) {
-      float4 w[OCH];
+      if (T + 1 < KT) {
 #pragma unroll
-      for (int o = 0; o < OCH; ++o) w[o] = lds[(o * KT + T) * WAVE + lane];
+        for (int o = 0; o < OCH; ++o) wn[o] = lds[(o * KT + T + 1) * WAVE + lane];
+      }
 #pragma unroll
-      for (int o = 0; o < OCH; ++o) acc[c * OCH + o] = mfma_k16(w[o], in[T], acc[c * OCH + o]);
+      for (int o = 0; o < OCH; ++o) acc[c * OCH + o] = mfma4(wc[o].x, in[T][0], acc[c * OCH + o]);
+#pragma unroll
+      for (int o = 0; o < OCH; ++o) acc[c * OCH + o] = mfma4(wc[o].y, in[T][1], acc[c * OCH + o]);
+#pragma unroll
+      for (int o = 0; o < OCH; ++o) acc[c * OCH + o] = mfma4(wc[o].z, in[T][2], acc[c * OCH + o]);
+#pragma unroll
+      for (int o = 0; o < OCH; ++o) acc[c * OCH + o] = mfma4(wc[o].w, in[T][3], acc[c * OCH + o]);
+      if (T + 1 < KT) {
+#pragma unroll
+        for (int o = 0; o < OCH; ++o) wc[o] = wn[o];
+      }
     }
+  }
+}
+
+// ---- pipelined weight stream ------------------------------------------------------------------
+// Two LDS buffers of kChunkKB each.  A layer's image is consumed in chunks of `och` output tiles; while
+// chunk i is multiplied, chunk i+1 (of this layer, or the first chunk of the NEXT layer) is already
+// landing in the other buffer by LDS-DMA, so the weight stream never stalls the MFMAs at a layer
+// boundary.  One barrier per chunk: it retires chunk i's DMA (the barrier's vmcnt(0)) and frees the
+// buffer chunk i-1 used.  `cnt` counts consumed chunks (buffer parity).
+constexpr int kChunkKB = 32;
+constexpr int kChunkF4 = kChunkKB * WAVE;          // float4 per buffer
+
+constexpr int chunk_och(int KT, int OT) {
+  int c = OT;
+  while (c > 1 && (c * KT > kChunkKB || OT % c != 0)) --c;
+  return c;
+}
+constexpr int chunk_f4(int KT, int OT) { return chunk_och(KT, OT) * KT * WAVE; }
+
+struct NoHook {
+  GNOT_DEV void operator()() const {}
+};
+
+template <int KT, int OT, typename Hook = NoHook>
+GNOT_DEV void mm_tiles_pipe(const float4* __restrict__ Wg, const float4* __restrict__ next_W, int next_f4,
+                            float4* lds, int& cnt, const float (&in)[KT][4], f32x4 (&acc)[OT], int nwaves,
+                            int wave, int lane, Hook hook = Hook()) {
+  constexpr int OCH = chunk_och(KT, OT);
+  constexpr int NC = OT / OCH;
+  constexpr int CH4 = OCH * KT * WAVE;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    __syncthreads();
+    float4* nb = lds + ((cnt + 1) & 1) * kChunkF4;
+    if (c + 1 < NC) stage_image(nb, Wg + (c + 1) * CH4, CH4, nwaves, wave, lane);
+    else if (next_W) stage_image(nb, next_W, next_f4, nwaves, wave, lane);
+    if (c + 1 == NC) hook();                           // e.g. prefetch the next layer's saved rows
+    const float4* cb = lds + (cnt & 1) * kChunkF4;
+    float4 wc[OCH], wn[OCH];
+#pragma unroll
+    for (int o = 0; o < OCH; ++o) wc[o] = cb[(o * KT + 0) * WAVE + lane];
+#pragma unroll
+    for (int T = 0; T < KT; ++T) {
+      if (T + 1 < KT) {
+#pragma unroll
+        for (int o = 0; o < OCH; ++o) wn[o] = cb[(o * KT + T + 1) * WAVE + lane];
+      }
+#pragma unroll
+      for (int o = 0; o < OCH; ++o) acc[c * OCH + o] = mfma4(wc[o].x, in[T][0], acc[c * OCH + o]);
+#pragma unroll
+      for (int o = 0; o < OCH; ++o) acc[c * OCH + o] = mfma4(wc[o].y, in[T][1], acc[c * OCH + o]);
+#pragma unroll
+      for (int o = 0; o < OCH; ++o) acc[c * OCH + o] = mfma4(wc[o].z, in[T][2], acc[c * OCH + o]);
+#pragma unroll
+      for (int o = 0; o < OCH; ++o) acc[c * OCH + o] = mfma4(wc[o].w, in[T][3], acc[c * OCH + o]);
+      if (T + 1 < KT) {
+#pragma unroll
+        for (int o = 0; o < OCH; ++o) wc[o] = wn[o];
+      }
+    }
+    ++cnt;
   }
 }
 

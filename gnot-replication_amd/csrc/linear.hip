@@ -15,8 +15,8 @@ namespace gnot {
 template <int D>
 __global__ void __launch_bounds__(256) linear_kernel(LinearArgs a) {
   constexpr int KT = D / 16;
-  constexpr int OC = lds_och(KT, (D / 16) < 8 ? (D / 16) : 8);   // output tiles per chunk (<= 64 KiB of W)
-  __shared__ __attribute__((aligned(16))) float4 wlds[OC * KT * WAVE];
+  constexpr int OC = lds_och(KT, (D / 16) < 8 ? (D / 16) : 8);   // output tiles per workgroup chunk
+  __shared__ __attribute__((aligned(16))) float4 wlds[2 * kChunkF4];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const long p = ((long)blockIdx.x * 4 + wave) * 16 + (lane & 15);
@@ -35,10 +35,16 @@ __global__ void __launch_bounds__(256) linear_kernel(LinearArgs a) {
 
   // grid.y splits the output chunks over workgroups (more parallelism at small point counts)
   const int nchunks = a.NO / (16 * OC);
+  int cnt = 0;
+  if ((int)blockIdx.y < nchunks)
+    stage_image(wlds, a.Wp + (long)blockIdx.y * OC * KT * WAVE, chunk_f4(KT, OC), 4, wave, lane);
   for (int c = blockIdx.y; c < nchunks; c += gridDim.y) {
     f32x4 acc[OC];
     init_bias<OC>(acc, a.bias ? a.bias + c * 16 * OC : nullptr, lane);
-    mm_tiles_lds<KT, OC>(a.Wp + (long)c * OC * KT * WAVE, wlds, in, acc, 4, wave, lane);
+    const bool more = c + (int)gridDim.y < nchunks;
+    mm_tiles_pipe<KT, OC>(a.Wp + (long)c * OC * KT * WAVE,
+                          more ? a.Wp + (long)(c + gridDim.y) * OC * KT * WAVE : nullptr, chunk_f4(KT, OC), wlds,
+                          cnt, in, acc, 4, wave, lane);
     float h[OC][4];
     acc_to_regs<OC>(acc, h);
     if (c * 16 * OC < a.nsoft) softmax_heads<OC>(h, a.dh);

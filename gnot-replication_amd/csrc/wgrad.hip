@@ -34,65 +34,36 @@ GNOT_DEV int find_job(const int* __restrict__ prefix, int njobs, int idx) {
   return lo;
 }
 
-// stage registers: thread t loads 4 float4 of A rows and 4 of B rows (32 rows x 32 float4 each)
+// Staging geometry: thread t owns column group c4 = t & 31 (columns 4*c4 .. 4*c4+3 of the tile) and
+// rows r0 + 8k (r0 = t >> 5, k = 0..3) of each 32-row stage, for both A and B.
 struct StageRegs {
   float4 a[4], b[4];
-  float wa[4];   // per-row weight for the A column sums (z / db), per float4
 };
 
-GNOT_DEV void stage_load(StageRegs& R, const WgradJob& J, long pbase, long pend, int c0o, int c0i, int tid) {
+GNOT_DEV float4 load4(const float* __restrict__ base, long p, long ld, int c, int ncols, bool pv) {
+  if (!pv) return make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c + 3 < ncols && (ld & 3) == 0) return *reinterpret_cast<const float4*>(base + p * ld + c);
+  float t[4];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int idx = tid + k * 256;          // 0..1023
-    const int row = idx >> 5, c4 = idx & 31;
-    const long p = pbase + row;
-    const bool pv = p < pend;
-    const int co = c0o + 4 * c4, ci = c0i + 4 * c4;
-    float4 va = make_float4(0.f, 0.f, 0.f, 0.f), vb = va;
-    if (pv) {
-      if (co + 3 < J.out && (J.lddz & 3) == 0) {
-        va = *reinterpret_cast<const float4*>(J.dz + p * J.lddz + co);
-      } else {
-        float t[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) t[r] = (co + r < J.out) ? J.dz[p * J.lddz + co + r] : 0.f;
-        va = make_float4(t[0], t[1], t[2], t[3]);
-      }
-      if (ci + 3 < J.in && (J.ldx & 3) == 0) {
-        vb = *reinterpret_cast<const float4*>(J.x + p * J.ldx + ci);
-      } else {
-        float t[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) t[r] = (ci + r < J.in) ? J.x[p * J.ldx + ci + r] : 0.f;
-        vb = make_float4(t[0], t[1], t[2], t[3]);
-      }
-    }
-    R.a[k] = va;
-    R.b[k] = vb;
-    R.wa[k] = 1.f;
-    if (J.w && pv && co < J.out) R.wa[k] = J.w[p * J.ldw + co / J.wdh];
-  }
+  for (int r = 0; r < 4; ++r) t[r] = (c + r < ncols) ? base[p * ld + c + r] : 0.f;
+  return make_float4(t[0], t[1], t[2], t[3]);
 }
 
-GNOT_DEV void stage_store(const StageRegs& R, const WgradJob& J, float* __restrict__ As, float* __restrict__ Bs,
-                          float* __restrict__ colw, int tid) {
+GNOT_DEV void stage_load(StageRegs& R, const WgradJob& J, long pbase, long pend, int co, int ci, int r0) {
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const int idx = tid + k * 256;
-    float4 vb = R.b[k];
-    if (J.x_gelu) { vb.x = gelu(vb.x); vb.y = gelu(vb.y); vb.z = gelu(vb.z); vb.w = gelu(vb.w); }
-    reinterpret_cast<float4*>(As)[idx] = R.a[k];
-    reinterpret_cast<float4*>(Bs)[idx] = vb;
-    if (J.w) colw[idx] = R.wa[k];     // weight of row (idx>>5) for A columns 4*(idx&31) .. +3
+    const long p = pbase + r0 + 8 * k;
+    const bool pv = p < pend;
+    R.a[k] = load4(J.dz, p, J.lddz, co, J.out, pv);
+    R.b[k] = load4(J.x, p, J.ldx, ci, J.in, pv);
   }
 }
 
 __global__ void __launch_bounds__(256) pgemm_kernel(const WgradJob* __restrict__ jobs, const int* __restrict__ prefix,
                                                     int njobs, float* __restrict__ slab) {
-  __shared__ __attribute__((aligned(16))) float smem[2 * kStage * kLdsRow + kStage * 32];
+  __shared__ __attribute__((aligned(16))) float smem[2 * kStage * kLdsRow];
   float* As = smem;
   float* Bs = smem + kStage * kLdsRow;
-  float* colw = Bs + kStage * kLdsRow;     // [32 rows][32 float4 groups]
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int j = find_job(prefix, njobs, blockIdx.x);
@@ -108,42 +79,60 @@ __global__ void __launch_bounds__(256) pgemm_kernel(const WgradJob* __restrict__
   const int c0o = to * kTile, c0i = ti * kTile;
   const int wo = wave >> 1, wi = wave & 1;      // 64x64 quadrant of this wave
   const int r32 = lane & 31, h = lane >> 5;
-  const bool want_db = (J.db != nullptr) && (wi == 0) && (J.diag_only || ti == 0);
+  const int c4 = tid & 31, r0 = tid >> 5;       // staging role
+  const int co = c0o + 4 * c4, ci = c0i + 4 * c4;
+  const bool want_db = (J.db != nullptr) && (J.diag_only || ti == 0);
+  const bool use_w = J.w != nullptr;
+  const bool gel = J.x_gelu != 0;
 
   f32x16 acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{};
-  float dbacc[2] = {0.f, 0.f};
+  float4 dbacc = make_float4(0.f, 0.f, 0.f, 0.f);   // column sums of this thread's A columns
 
   StageRegs R;
-  if (pb < pe) stage_load(R, J, pb, pe, c0o, c0i, tid);
+  if (pb < pe) stage_load(R, J, pb, pe, co, ci, r0);
   for (long p0 = pb; p0 < pe; p0 += kStage) {
     __syncthreads();                          // previous stage fully consumed
-    stage_store(R, J, As, Bs, colw, tid);
-    __syncthreads();
-    if (p0 + kStage < pe) stage_load(R, J, p0 + kStage, pe, c0o, c0i, tid);   // in flight during MFMAs
-#pragma unroll 4
-    for (int s = 0; s < kStage / 2; ++s) {
-      const int row = 2 * s + h;
-      const float* ar = As + row * kLdsRow + wo * 64 + r32;
-      const float* br = Bs + row * kLdsRow + wi * 64 + r32;
-      const float a0 = ar[0], a1 = ar[32];
-      const float b0 = br[0], b1 = br[32];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int row = r0 + 8 * k;
+      float4 vb = R.b[k];
+      if (gel) { vb.x = gelu(vb.x); vb.y = gelu(vb.y); vb.z = gelu(vb.z); vb.w = gelu(vb.w); }
+      reinterpret_cast<float4*>(As)[row * 32 + c4] = R.a[k];
+      reinterpret_cast<float4*>(Bs)[row * 32 + c4] = vb;
       if (want_db) {
-        if (J.w) {
-          const float* wr = colw + row * 32;
-          dbacc[0] = fmaf(wr[(wo * 64 + r32) >> 2], a0, dbacc[0]);
-          dbacc[1] = fmaf(wr[(wo * 64 + 32 + r32) >> 2], a1, dbacc[1]);
-        } else {
-          dbacc[0] += a0;
-          dbacc[1] += a1;
-        }
+        const long p = p0 + row;
+        const float wgt = (use_w && p < pe && co < J.out) ? J.w[p * J.ldw + co / J.wdh] : 1.f;
+        dbacc.x = fmaf(wgt, R.a[k].x, dbacc.x);
+        dbacc.y = fmaf(wgt, R.a[k].y, dbacc.y);
+        dbacc.z = fmaf(wgt, R.a[k].z, dbacc.z);
+        dbacc.w = fmaf(wgt, R.a[k].w, dbacc.w);
+      }
+    }
+    __syncthreads();
+    if (p0 + kStage < pe) stage_load(R, J, p0 + kStage, pe, co, ci, r0);   // in flight during MFMAs
+    // 16 k-steps (2 points each) in four batches of 4: fragment reads first, then 16 MFMAs
+#pragma unroll
+    for (int half = 0; half < 4; ++half) {
+      float a0[4], a1[4], b0[4], b1[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int row = 2 * (4 * half + s) + h;
+        const float* ar = As + row * kLdsRow + wo * 64 + r32;
+        const float* br = Bs + row * kLdsRow + wi * 64 + r32;
+        a0[s] = ar[0]; a1[s] = ar[32];
+        b0[s] = br[0]; b1[s] = br[32];
+      }
+      __builtin_amdgcn_sched_barrier(0);   // keep the 8 LDS reads batched ahead of the 16 MFMAs
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], b0[s], acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[s], b1[s], acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b0[s], acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[s], b1[s], acc[1][1], 0, 0, 0);
       }
     }
   }
@@ -163,10 +152,21 @@ __global__ void __launch_bounds__(256) pgemm_kernel(const WgradJob* __restrict__
         S[row * (kTile + 1) + col] = acc[a][b][r];
       }
   if (want_db) {
+    // sum the 8 row-owners of every column group through LDS (reuses the A stage buffer)
+    __syncthreads();
+    reinterpret_cast<float4*>(As)[r0 * 32 + c4] = dbacc;
+    __syncthreads();
+    if (r0 == 0) {
+      float4 tot = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int a = 0; a < 2; ++a) {
-      const float v = dbacc[a] + __shfl_xor(dbacc[a], 32, 64);
-      if (h == 0) S[(wo * 64 + a * 32 + r32) * (kTile + 1) + kTile] = v;
+      for (int k = 0; k < 8; ++k) {
+        const float4 v = reinterpret_cast<const float4*>(As)[k * 32 + c4];
+        tot.x += v.x; tot.y += v.y; tot.z += v.z; tot.w += v.w;
+      }
+      S[(4 * c4 + 0) * (kTile + 1) + kTile] = tot.x;
+      S[(4 * c4 + 1) * (kTile + 1) + kTile] = tot.y;
+      S[(4 * c4 + 2) * (kTile + 1) + kTile] = tot.z;
+      S[(4 * c4 + 3) * (kTile + 1) + kTile] = tot.w;
     }
   }
 }
