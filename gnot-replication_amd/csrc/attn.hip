@@ -177,8 +177,7 @@ __global__ void __launch_bounds__(256) attn_apply_bwd_kernel(AttnApplyArgs a) {
 
 // ---------------------------------------------------------------- K/V backward
 template <int DH>
-__global__ void __launch_bounds__(256) attn_kv_bwd_kernel(AttnKVBwdArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
+GNOT_DEV void attn_kv_bwd_body(const AttnKVBwdArgs& a, float* smem) {
   const int4 ch = a.chunks[blockIdx.x];
   const int b = ch.x;
   const int H = a.H;
@@ -216,6 +215,20 @@ __global__ void __launch_bounds__(256) attn_kv_bwd_kernel(AttnKVBwdArgs a) {
       *reinterpret_cast<float4*>(dvp + j) = make_float4(dv[j], dv[j + 1], dv[j + 2], dv[j + 3]);
     }
   }
+}
+
+template <int DH>
+__global__ void __launch_bounds__(256) attn_kv_bwd_kernel(AttnKVBwdArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  attn_kv_bwd_body<DH>(a, smem);
+}
+
+template <int DH>
+__global__ void __launch_bounds__(256) attn_kv_bwd_batch_kernel(const AttnKVBwdArgs* __restrict__ jobs) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const AttnKVBwdArgs a = jobs[blockIdx.y];
+  if ((int)blockIdx.x >= a.nchunks) return;
+  attn_kv_bwd_body<DH>(a, smem);
 }
 
 #define GNOT_DH_SWITCH(DHV, ...)        \
@@ -257,6 +270,15 @@ hipError_t launch_attn_kv_bwd(const AttnKVBwdArgs& a, hipStream_t s) {
   const size_t lds = (size_t)a.H * (a.dh * a.dh + a.dh) * sizeof(float);
   GNOT_DH_SWITCH(a.dh, allow_lds(attn_kv_bwd_kernel<DH>, lds);
                  hipLaunchKernelGGL(attn_kv_bwd_kernel<DH>, dim3(a.nchunks), dim3(256), lds, s, a));
+  return hipGetLastError();
+}
+
+hipError_t launch_attn_kv_bwd_batch(const AttnKVBwdArgs* jobs_dev, int njobs, int maxchunks, int H, int dh,
+                                    hipStream_t s) {
+  if (njobs <= 0 || maxchunks <= 0) return hipSuccess;
+  const size_t lds = (size_t)H * (dh * dh + dh) * sizeof(float);
+  GNOT_DH_SWITCH(dh, allow_lds(attn_kv_bwd_batch_kernel<DH>, lds);
+                 hipLaunchKernelGGL(attn_kv_bwd_batch_kernel<DH>, dim3(maxchunks, njobs), dim3(256), lds, s, jobs_dev));
   return hipGetLastError();
 }
 

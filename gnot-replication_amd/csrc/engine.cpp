@@ -126,6 +126,15 @@ struct gnot_plan {
   std::vector<WgradGroup> wg_m1, wg_m2, wg_self, wg_cross;
   // attention states as point-reduction GEMM jobs (one job per sample)
   std::vector<std::vector<WgradGroup>> st_c, dst_c;   // [l][source i]
+  // cross attention with input functions: the input-function side of EVERY block is batched
+  WgradGroup st_fn;                                    // forward states of all (block, fn, sample)
+  WgradGroup wg_fnkv;                                  // weight grads of all key/value projections
+  std::vector<LinearArgs> fwd_kv_jobs;                 // key/value projections of all (block, fn)
+  std::vector<AttnKVBwdArgs> kvbwd_jobs;               // dK/dV of all (block, fn)
+  std::vector<std::vector<LinearArgs>> dfn_jobs;       // d(fn encoding): launches of <= kMaxSeg segments
+  LinearArgs* d_fwd_kv_jobs = nullptr;
+  AttnKVBwdArgs* d_kvbwd_jobs = nullptr;
+  std::vector<LinearArgs*> d_dfn_jobs;
   std::vector<WgradGroup> st_s, dst_s;                 // [l]
   size_t table_bytes = 0;
   size_t slab_wgrad_floats = 0, slab_state_floats = 0;
@@ -190,7 +199,8 @@ struct gnot_plan {
   int k_gate() const { return 2 + 2 * L + I; }
   std::string dsum_buf(bool m1) const { return m1 ? "dsum1" : "dsum0"; }
   std::string dqkv_buf(bool cross) const { return cross ? "dqkv1" : "dqkv0"; }
-  std::string dkv_buf(int l, int i) const { return "dkv" + std::to_string(i) + "_" + std::to_string((L - 1 - l) & 1); }
+  std::string dkv_buf(int l, int i) const { return "dkv" + std::to_string(l) + "_" + std::to_string(i); }
+  std::string dstate_fn(int l, int i) const { return "dstate" + std::to_string(l) + "_" + std::to_string(i); }
   float* P_(const char* name) const { return bufs.at(name).p; }
   float* P_(const std::string& name) const { return bufs.at(name).p; }
 };
@@ -467,7 +477,9 @@ static void for_each_group(gnot_plan* p, F&& f) {
     f(p->wg_out); f(p->wg_x); f(p->wg_gate);
     for (auto& G : p->wg_fn) f(G);
     for (int l = 0; l < p->L; ++l) { f(p->wg_m1[l]); f(p->wg_m2[l]); f(p->wg_self[l]); f(p->wg_cross[l]); }
+    f(p->wg_fnkv);
   }
+  f(p->st_fn);
   for (int l = 0; l < p->L; ++l) {
     for (auto& G : p->st_c[l]) f(G);
     f(p->st_s[l]);
@@ -539,11 +551,7 @@ static void build_groups(gnot_plan* p) {
     const std::string s = "b" + std::to_string(l) + ".";
     // forward states
     if (I > 0) {
-      for (int i = 0; i < I; ++i) {
-        const std::string si = std::to_string(i);
-        float* kv = p->P_(s + "ckv" + si);
-        state_group(p->st_c[l][i], kv, 2 * D, kv + D, 2 * D, nullptr, 0, p->fnoff[i], p->P_(s + "cstate" + si));
-      }
+      // (all blocks' input-function states are one group: st_fn, below)
     } else {
       float* qkv = p->P_(s + "cq");
       state_group(p->st_c[l][0], qkv + D, 3 * D, qkv + 2 * D, 3 * D, nullptr, 0, p->xoff, p->P_(s + "cstate0"));
@@ -558,12 +566,43 @@ static void build_groups(gnot_plan* p) {
       const std::string si = std::to_string(i);
       const long ldq = I > 0 ? D : 3 * D;
       state_group(p->dst_c[l][i], p->P_(s + "cq"), ldq, p->P_("du" + si), D, p->P_("dden" + si), p->H, p->xoff,
-                  p->P_("dstate" + si));
+                  p->P_(I > 0 ? p->dstate_fn(l, i) : std::string("dstate0")));
     }
     state_group(p->dst_s[l], p->P_(s + "sq"), 3 * D, p->P_("du0"), D, p->P_("dden0"), p->H, p->xoff,
                 p->P_("dstate0"));
   }
+  p->st_fn = {};
+  if (I > 0) {
+    // one job per (block, fn, sample): S = k^T v, z = sum k over that sample's input-function points
+    for (int l = 0; l < p->L; ++l)
+      for (int i = 0; i < I; ++i) {
+        const std::string s = "b" + std::to_string(l) + ".", si = std::to_string(i);
+        float* kv = p->P_(s + "ckv" + si);
+        float* st = p->P_(s + "cstate" + si);
+        for (int b = 0; b < p->B; ++b) {
+          WgradJob J{};
+          const long o = p->fnoff[i][b];
+          J.dz = kv + o * 2 * D; J.lddz = 2 * D; J.x = kv + D + o * 2 * D; J.ldx = 2 * D;
+          J.out = D; J.in = D; J.dW = st + b * per_state; J.db = J.dW; J.wdh = dh;
+          J.state_dh = dh; J.diag_only = 1; J.P = (int)(p->fnoff[i][b + 1] - o);
+          p->st_fn.jobs.push_back(J);
+        }
+      }
+    finish_group(p, p->st_fn);
+  }
   if (!tr) return;
+
+  p->wg_fnkv = {};
+  if (I > 0) {
+    for (int l = 0; l < p->L; ++l)
+      for (int i = 0; i < I; ++i) {
+        float* dkv = p->P_(p->dkv_buf(l, i));
+        const float* enc = p->P_("fnenc" + std::to_string(i));
+        lin_job(p->wg_fnkv, p->lin_ck(l, i), dkv, 2 * D, enc, D, 0, p->Q[i]);
+        lin_job(p->wg_fnkv, p->lin_cv(l, i), dkv + D, 2 * D, enc, D, 0, p->Q[i]);
+      }
+    finish_group(p, p->wg_fnkv);
+  }
 
   chain_group(p->wg_out, p->k_out(), {p->lin_out(0)}, P, p->P_(p->final_query()), D, p->P_("out_save"));
   chain_group(p->wg_x, p->k_x(), {p->lin_x(0)}, P, p->P_("xin"), p->bufs.at("xin").ld, p->P_("x_save"));
@@ -597,13 +636,7 @@ static void build_groups(gnot_plan* p) {
       const float* qin = p->P_(p->block_query(l));
       lin_job(G, p->lin_co(l), dsum, D, p->P_(s + "cres"), D, 0, P);
       if (I > 0) {
-        lin_job(G, p->lin_cq(l), dqkv, D, qin, D, 0, P);
-        for (int i = 0; i < I; ++i) {
-          const std::string si = std::to_string(i);
-          float* dkv = p->P_(p->dkv_buf(l, i));
-          lin_job(G, p->lin_ck(l, i), dkv, 2 * D, p->P_("fnenc" + si), D, 0, p->Q[i]);
-          lin_job(G, p->lin_cv(l, i), dkv + D, 2 * D, p->P_("fnenc" + si), D, 0, p->Q[i]);
-        }
+        lin_job(G, p->lin_cq(l), dqkv, D, qin, D, 0, P);   // key/value grads: wg_fnkv
       } else {
         lin_job(G, p->lin_cq(l), dqkv, 3 * D, qin, D, 0, P);
         lin_job(G, p->lin_ck(l, 0), dqkv + D, 3 * D, qin, D, 0, P);
@@ -611,6 +644,58 @@ static void build_groups(gnot_plan* p) {
       }
       finish_group(p, G);
     }
+  }
+}
+
+// Device job tables of the batched input-function side of cross attention (pointers are null
+// before bind: sizing only).
+static void build_attn_tables(gnot_plan* p) {
+  const int D = p->D, I = p->I, L = p->L;
+  p->fwd_kv_jobs.clear();
+  p->kvbwd_jobs.clear();
+  p->dfn_jobs.clear();
+  if (I == 0 || L == 0) return;
+  float* pbias = p->P_("pbias");
+  for (int l = 0; l < L; ++l)
+    for (int i = 0; i < I; ++i) {
+      const std::string s = "b" + std::to_string(l) + ".", si = std::to_string(i);
+      const gnot_plan::AttnImgs& A = p->cross_img[l];
+      LinearArgs a{};
+      a.nseg = 1; a.X[0] = p->P_("fnenc" + si); a.ldx = D; a.Wp[0] = A.kv[i].p; a.nsum = 1; a.K = D;
+      a.bias = pbias + A.bkv[i]; a.Y = p->P_(s + "ckv" + si); a.ldy = 2 * D; a.NO = 2 * D; a.P = (int)p->Q[i];
+      a.epi = EPI_STORE; a.nsoft = D; a.dh = p->dh;
+      p->fwd_kv_jobs.push_back(a);
+    }
+  if (!p->training) return;
+  for (int l = 0; l < L; ++l)
+    for (int i = 0; i < I; ++i) {
+      const std::string s = "b" + std::to_string(l) + ".";
+      const float* kv = p->P_(s + "ckv" + std::to_string(i));
+      float* dkv = p->P_(p->dkv_buf(l, i));
+      AttnKVBwdArgs kb{};
+      kb.k = kv; kb.v = kv + D; kb.ldkv = 2 * D; kb.dstate = p->P_(p->dstate_fn(l, i));
+      kb.chunks = p->d_fchunks.empty() ? nullptr : p->d_fchunks[i];
+      kb.nchunks = (int)p->fchunks[i].size(); kb.H = p->H; kb.dh = p->dh;
+      kb.dk = dkv; kb.dv = dkv + D; kb.lddkv = 2 * D;
+      p->kvbwd_jobs.push_back(kb);
+    }
+  // d(fn encoding i) = sum_l dK_{l,i} Wk_{l,i} + dV_{l,i} Wv_{l,i}: 2L K-segments, <= kMaxSeg per launch
+  const int nseg = 2 * L;
+  for (int k0 = 0; k0 < nseg; k0 += kMaxSeg) {
+    std::vector<LinearArgs> launch;
+    for (int i = 0; i < I; ++i) {
+      LinearArgs a{};
+      a.nseg = std::min(kMaxSeg, nseg - k0);
+      for (int sg = 0; sg < a.nseg; ++sg) {
+        const int l = (k0 + sg) / 2, kv = (k0 + sg) % 2;
+        a.X[sg] = p->P_(p->dkv_buf(l, i)) + kv * D;
+        a.Wp[sg] = p->T_img[kv ? p->lin_cv(l, i) : p->lin_ck(l, i)].p;
+      }
+      a.ldx = 2 * D; a.nsum = 1; a.K = D; a.bias = nullptr; a.Y = p->P_("dfn" + std::to_string(i)); a.ldy = D;
+      a.NO = D; a.P = (int)p->Q[i]; a.epi = k0 == 0 ? EPI_STORE : EPI_ACCUM; a.nsoft = 0; a.dh = p->dh;
+      launch.push_back(a);
+    }
+    p->dfn_jobs.push_back(launch);
   }
 }
 
@@ -715,11 +800,14 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
     for (int i = 0; i < KI; ++i) {
       C.add("du" + std::to_string(i), P * D, D);
       C.add("dden" + std::to_string(i), P * H, H);
-      C.add("dstate" + std::to_string(i), p->B * per_state, per_state);
     }
+    C.add("dstate0", p->B * per_state, per_state);
+    for (int l = 0; l < p->L; ++l)
+      for (int i = 0; i < I; ++i) {
+        C.add(p->dstate_fn(l, i), p->B * per_state, per_state);
+        C.add(p->dkv_buf(l, i), p->Q[i] * 2 * D, 2 * D);
+      }
     for (int i = 0; i < I; ++i) {
-      C.add("dkv" + std::to_string(i) + "_0", p->Q[i] * 2 * D, 2 * D);
-      C.add("dkv" + std::to_string(i) + "_1", p->Q[i] * 2 * D, 2 * D);
       C.add("dfn" + std::to_string(i), p->Q[i] * D, D);
     }
     C.add("dz0", E * NL * std::max(P, Qmax) * D, D);
@@ -774,6 +862,10 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
     tbl(G.jobs.size() * sizeof(int) * 2);
   };
   for_each_group(p, tbl_group);
+  build_attn_tables(p);
+  tbl(p->fwd_kv_jobs.size() * sizeof(LinearArgs));
+  tbl(p->kvbwd_jobs.size() * sizeof(AttnKVBwdArgs));
+  for (auto& v : p->dfn_jobs) tbl(v.size() * sizeof(LinearArgs));
   C.add("slab_wgrad", p->slab_wgrad_floats, 0);
   C.add("slab_state", p->slab_state_floats, 0);
   const size_t table_off = C.raw(p->table_bytes);
@@ -887,6 +979,11 @@ extern "C" int gnot_plan_bind_workspace(gnot_plan* p, void* workspace, size_t by
       G.d_red_prefix = d + G.jobs.size();
     });
   }
+  build_attn_tables(p);
+  p->d_fwd_kv_jobs = static_cast<LinearArgs*>(put(p->fwd_kv_jobs.data(), p->fwd_kv_jobs.size() * sizeof(LinearArgs)));
+  p->d_kvbwd_jobs = static_cast<AttnKVBwdArgs*>(put(p->kvbwd_jobs.data(), p->kvbwd_jobs.size() * sizeof(AttnKVBwdArgs)));
+  p->d_dfn_jobs.clear();
+  for (auto& v : p->dfn_jobs) p->d_dfn_jobs.push_back(static_cast<LinearArgs*>(put(v.data(), v.size() * sizeof(LinearArgs))));
   if (cur > p->table_bytes) return fail(GNOT_E_INVALID, "internal: table overflow");
   GNOT_CK(hipMemcpy(tp, host.data(), cur, hipMemcpyHostToDevice));
   if (p->training && !p->side) GNOT_CK(hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
@@ -945,9 +1042,25 @@ struct ProfScope {
 int run_linear(Ctx& c, const float* X, long ldx, int K, const Img& A, const float* bias, float* Y, long ldy,
                int NO, long P, int epi, int nsoft) {
   LinearArgs a{};
-  a.X = X; a.ldx = ldx; a.nsum = 1; a.sum_stride = 0; a.K = K;
-  a.Wp = A.p; a.bias = bias; a.Y = Y; a.ldy = ldy; a.NO = NO; a.P = (int)P;
+  a.nseg = 1; a.X[0] = X; a.Wp[0] = A.p; a.ldx = ldx; a.nsum = 1; a.sum_stride = 0; a.K = K;
+  a.bias = bias; a.Y = Y; a.ldy = ldy; a.NO = NO; a.P = (int)P;
   a.epi = epi; a.nsoft = nsoft; a.dh = c.p->dh;
+  GNOT_CK(launch_linear(a, c.p->D, c.s));
+  return GNOT_OK;
+}
+
+// Y (+)= sum_s X_s A_s over K-segments that share one row pitch (backward-data of several Linears)
+int run_linear_seg(Ctx& c, std::initializer_list<std::pair<const float*, const Img*>> segs, long ldx, float* Y,
+                   long ldy, long P, int epi) {
+  LinearArgs a{};
+  a.nseg = 0;
+  for (const auto& sg : segs) {
+    a.X[a.nseg] = sg.first;
+    a.Wp[a.nseg] = sg.second->p;
+    ++a.nseg;
+  }
+  a.ldx = ldx; a.nsum = 1; a.K = c.p->D; a.bias = nullptr; a.Y = Y; a.ldy = ldy; a.NO = c.p->D; a.P = (int)P;
+  a.epi = epi; a.nsoft = 0; a.dh = c.p->dh;
   GNOT_CK(launch_linear(a, c.p->D, c.s));
   return GNOT_OK;
 }
@@ -1028,14 +1141,8 @@ int attn_forward(Ctx& c, int l, bool cross, const float* q_in, float* res_out, f
     float* q = p->P_(s + "cq");
     GNOT_RUN(run_linear(c, q_in, D, D, A.q, pbias + A.bq, q, D, D, P, EPI_STORE, D));
     AttnApplyArgs ap{};
-    for (int i = 0; i < p->I; ++i) {
-      const std::string si = std::to_string(i);
-      float* kv = p->P_(s + "ckv" + si);
-      GNOT_RUN(run_linear(c, p->P_("fnenc" + si), D, D, A.kv[i], pbias + A.bkv[i], kv, 2 * D, 2 * D, p->Q[i],
-                          EPI_STORE, D));
-      GNOT_RUN(run_state(c, p->st_c[l][i]));
-      ap.state[i] = p->P_(s + "cstate" + si);
-    }
+    // keys/values/states of the input functions were computed for every block up front
+    for (int i = 0; i < p->I; ++i) ap.state[i] = p->P_(s + "cstate" + std::to_string(i));
     ap.q = q; ap.ldq = D; ap.nsrc = p->I; ap.chunks = p->d_qchunks; ap.nchunks = nq; ap.off = p->d_xoff;
     ap.H = p->H; ap.dh = p->dh; ap.res = res_out;
     GNOT_CK(launch_attn_apply_fwd(ap, c.s));
@@ -1082,27 +1189,10 @@ int attn_backward(Ctx& c, int l, bool cross) {
       ap.dden[i] = p->P_("dden" + si);
     }
     GNOT_CK(launch_attn_apply_bwd(ap, c.s));
-    std::vector<const float*> dkvs;
-    for (int i = 0; i < p->I; ++i) {
-      const std::string si = std::to_string(i);
-      float* dst = p->P_("dstate" + si);
-      GNOT_RUN(run_state(c, p->dst_c[l][i]));
-      const float* kv = p->P_(s + "ckv" + si);
-      float* dkv = p->P_(p->dkv_buf(l, i));
-      GNOT_RUN(guard_write(c, dkv));
-      AttnKVBwdArgs kb{};
-      kb.k = kv; kb.v = kv + D; kb.ldkv = 2 * D; kb.dstate = dst; kb.chunks = p->d_fchunks[i];
-      kb.nchunks = (int)p->fchunks[i].size(); kb.H = p->H; kb.dh = p->dh; kb.dk = dkv; kb.dv = dkv + D;
-      kb.lddkv = 2 * D;
-      GNOT_CK(launch_attn_kv_bwd(kb, c.s));
-      float* dfn = p->P_("dfn" + si);
-      GNOT_RUN(run_linear(c, dkv, 2 * D, D, p->T_img[p->lin_ck(l, i)], nullptr, dfn, D, D, p->Q[i], EPI_ACCUM, 0));
-      GNOT_RUN(run_linear(c, dkv + D, 2 * D, D, p->T_img[p->lin_cv(l, i)], nullptr, dfn, D, D, p->Q[i], EPI_ACCUM, 0));
-      dkvs.push_back(dkv);
-    }
+    // dS, dz per input function (kept per block: the dK/dV side of every block runs batched later)
+    for (int i = 0; i < p->I; ++i) GNOT_RUN(run_state(c, p->dst_c[l][i]));
     GNOT_RUN(run_linear(c, dqkv, D, D, p->T_img[lq], nullptr, dquery, D, D, P, EPI_ACCUM, 0));
     GNOT_RUN(run_wgrad_side(c, p->wg_cross[l], {dsum, dqkv}));
-    for (const float* d : dkvs) p->readers[d] = p->readers[dsum];
   } else {
     const float* qkv = p->P_(cross ? s + "cq" : s + "sq");
     const int lk = cross ? p->lin_ck(l, 0) : p->lin_sk(l);
@@ -1119,9 +1209,8 @@ int attn_backward(Ctx& c, int l, bool cross) {
     kb.k = qkv + D; kb.v = qkv + 2 * D; kb.ldkv = 3 * D; kb.dstate = dst; kb.chunks = p->d_qchunks;
     kb.nchunks = nq; kb.H = p->H; kb.dh = p->dh; kb.dk = dqkv + D; kb.dv = dqkv + 2 * D; kb.lddkv = 3 * D;
     GNOT_CK(launch_attn_kv_bwd(kb, c.s));
-    GNOT_RUN(run_linear(c, dqkv, 3 * D, D, p->T_img[lq], nullptr, dquery, D, D, P, EPI_ACCUM, 0));
-    GNOT_RUN(run_linear(c, dqkv + D, 3 * D, D, p->T_img[lk], nullptr, dquery, D, D, P, EPI_ACCUM, 0));
-    GNOT_RUN(run_linear(c, dqkv + 2 * D, 3 * D, D, p->T_img[lv], nullptr, dquery, D, D, P, EPI_ACCUM, 0));
+    GNOT_RUN(run_linear_seg(c, {{dqkv, &p->T_img[lq]}, {dqkv + D, &p->T_img[lk]}, {dqkv + 2 * D, &p->T_img[lv]}},
+                            3 * D, dquery, D, P, EPI_ACCUM));
     GNOT_RUN(run_wgrad_side(c, cross ? p->wg_cross[l] : p->wg_self[l], {dsum, dqkv}));
   }
   return GNOT_OK;
@@ -1173,6 +1262,14 @@ extern "C" int gnot_forward(gnot_plan* p, const float* x, const float* theta, co
     a.Y = p->P_("fnenc" + si); a.ldy = D; a.mode = CH_STORE;
     if (tr) { a.save = p->P_("fn_save" + si); a.save_layer_stride = p->Q[i] * D; a.save_chain_stride = NL * p->Q[i] * D; }
     GNOT_CK(launch_chain_fwd(a, c.s));
+  }
+  // key/value projections (model.py:67-75) and states (model.py:77-79) of every (block, input
+  // function): they depend only on the input-function encodings, so all L*I of them run batched here
+  if (p->I > 0 && p->L > 0) {
+    long Qmax = 0;
+    for (long q : p->Q) Qmax = std::max(Qmax, q);
+    GNOT_CK(launch_linear_batch(p->d_fwd_kv_jobs, (int)p->fwd_kv_jobs.size(), (int)Qmax, 2 * D, D, c.s));
+    GNOT_RUN(run_state(c, p->st_fn));
   }
   // blocks (model.py:126-139)
   for (int l = 0; l < p->L; ++l) {
@@ -1227,8 +1324,6 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
   GNOT_CK(hipMemcpy2DAsync(p->P_("dout"), p->bufs["dout"].ld * 4, dout, p->out * 4, p->out * 4, P,
                            hipMemcpyDeviceToDevice, c.s));
   GNOT_CK(hipMemsetAsync(p->P_("dscore"), 0, P * p->bufs["dscore"].ld * 4, c.s));
-  for (int i = 0; i < p->I; ++i)
-    GNOT_CK(hipMemsetAsync(p->P_("dfn" + std::to_string(i)), 0, p->Q[i] * D * 4, c.s));
   // one chain backward: dZ of every Linear into the chain call's dz slot, then its weight gradients
   // are forked to the side stream
   auto chain_bwd = [&](ChainArgs& a, int kcall, long rows, const WgradGroup& G, const char* prof) -> int {
@@ -1267,6 +1362,23 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
       GNOT_RUN(attn_backward(c, l, m1));
     }
   }
+  // dK, dV of every (block, input function), the encodings' gradient and the key/value weight
+  // gradients, batched over blocks
+  if (p->I > 0 && p->L > 0) {
+    long Qmax = 0;
+    int maxch = 0;
+    for (int i = 0; i < p->I; ++i) {
+      Qmax = std::max(Qmax, p->Q[i]);
+      maxch = std::max(maxch, (int)p->fchunks[i].size());
+    }
+    GNOT_CK(launch_attn_kv_bwd_batch(p->d_kvbwd_jobs, (int)p->kvbwd_jobs.size(), maxch, p->H, p->dh, c.s));
+    for (size_t k = 0; k < p->d_dfn_jobs.size(); ++k)
+      GNOT_CK(launch_linear_batch(p->d_dfn_jobs[k], p->I, (int)Qmax, D, D, c.s));
+    GNOT_RUN(run_wgrad_side(c, p->wg_fnkv, {}));
+  }
+  if (p->I > 0 && p->L == 0)   // encodings unused by the output: zero gradients
+    for (int i = 0; i < p->I; ++i)
+      GNOT_CK(hipMemsetAsync(p->P_("dfn" + std::to_string(i)), 0, p->Q[i] * D * 4, c.s));
   // input-function encoders (their inputs need no gradient)
   for (int i = 0; i < p->I; ++i) {
     const std::string si = std::to_string(i);

@@ -27,23 +27,27 @@ hipError_t launch_pack(const PackJob* jobs_dev, const int* tile_prefix_dev, int 
 
 // ------------------------------------------------------------------ projections (linear.hip)
 enum LinearEpi { EPI_STORE = 0, EPI_ACCUM = 1 };
+constexpr int kMaxSeg = 8;
 struct LinearArgs {
-  const float* X;      // input rows: sum_{s<nsum} X[s*sum_stride + p*ldx + f]
+  int nseg;                          // K-segments: Y = sum_s X[s] . A_s (+ bias)
+  const float* X[kMaxSeg];           // segment input rows X[s] + p*ldx, K columns each
+  const float4* Wp[kMaxSeg];         // segment packed A images (NO/16 x ceil(K/16) tiles)
   long ldx;
-  int nsum;
+  int nsum;                          // segment 0 only: input = sum_{t<nsum} X[0][t*sum_stride + ...]
   long sum_stride;
-  int K;               // real input columns (<= 16*KT)
-  const float4* Wp;    // packed A operand, KT = ceil(K/16) tiles per output tile
-  const float* bias;   // padded bias or null
+  int K;                             // real input columns (<= D)
+  const float* bias;                 // padded bias or null
   float* Y;
   long ldy;
-  int NO;              // output columns (multiple of 16)
-  int P;               // rows
-  int epi;             // LinearEpi
-  int nsoft;           // feature-softmax on output columns [0, nsoft)
-  int dh;              // head width for that softmax
+  int NO;                            // output columns (multiple of D)
+  int P;                             // rows
+  int epi;                           // LinearEpi
+  int nsoft;                         // feature-softmax on output columns [0, nsoft)
+  int dh;                            // head width for that softmax
 };
-hipError_t launch_linear(const LinearArgs& a, int D, hipStream_t s);   // K <= D, NO % D == 0
+hipError_t launch_linear(const LinearArgs& a, int D, hipStream_t s);
+// jobs_dev: device array of independent LinearArgs (same D and NO), one per grid.z
+hipError_t launch_linear_batch(const LinearArgs* jobs_dev, int njobs, int maxP, int NO, int D, hipStream_t s);
 
 // ------------------------------------------------------------------ fused MLP chains (chain.hip)
 enum ChainMode { CH_STORE = 0, CH_SOFTMAX = 1, CH_MOE = 2 };
@@ -124,6 +128,9 @@ struct AttnKVBwdArgs {
   float* dk; float* dv; long lddkv;  // pre-softmax dK, dV
 };
 hipError_t launch_attn_kv_bwd(const AttnKVBwdArgs& a, hipStream_t s);
+// independent K/V backward jobs (every block x input function) in one launch, job = grid.y
+hipError_t launch_attn_kv_bwd_batch(const AttnKVBwdArgs* jobs_dev, int njobs, int maxchunks, int H, int dh,
+                                    hipStream_t s);
 
 // ------------------------------------------------------------------ small elementwise (misc.hip)
 hipError_t launch_concat_theta(const float* x, long ldx, int in_dim, const float* theta, int th_dim,

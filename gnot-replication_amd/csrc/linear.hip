@@ -6,72 +6,117 @@
 // (gnot_common.h), the input row block is loaded ONCE and reused for all NO output columns; the
 // A operand is the packed weight image streamed from L2 (one 1 KiB load per 4 MFMAs).
 // The input may be a sum of `nsum` equally strided buffers (the per-expert dX stage of the MoE
-// backward), which fuses the expert reduction into the consumer.
+// backward), and the contraction may run over several K-segments with their own input rows and
+// weight images (backward-data of the q/k/v projections: dX = dQ Wq + dK Wk + dV Wv in one pass).
+// A batched variant runs independent jobs (e.g. the key/value projections of every block and
+// input function) in one launch.
 #include "gnot_common.h"
 #include "gnot_kernels.h"
 
 namespace gnot {
 
 template <int D>
-__global__ void __launch_bounds__(256) linear_kernel(LinearArgs a) {
+GNOT_DEV void linear_body(const LinearArgs& a, float4* wlds) {
   constexpr int KT = D / 16;
   constexpr int OC = lds_och(KT, (D / 16) < 8 ? (D / 16) : 8);   // output tiles per workgroup chunk
-  __shared__ __attribute__((aligned(16))) float4 wlds[2 * kChunkF4];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const long p = ((long)blockIdx.x * 4 + wave) * 16 + (lane & 15);
   const bool valid = p < a.P;
+  const int c = blockIdx.y;                       // output chunk of this workgroup
+  const long wchunk = (long)c * OC * KT * WAVE;   // chunk offset inside every segment's image
+  int cnt = 0;
+  stage_image(wlds, a.Wp[0] + wchunk, chunk_f4(KT, OC), 4, wave, lane);
 
+  // segment 0 input (optionally the sum of nsum equally strided buffers)
   float in[KT][4];
-  load_rows<KT>(in, a.X, a.ldx, p, valid, a.K, lane);
+  load_rows<KT>(in, a.X[0], a.ldx, p, valid, a.K, lane);
   for (int s = 1; s < a.nsum; ++s) {
     float t[KT][4];
-    load_rows<KT>(t, a.X + s * a.sum_stride, a.ldx, p, valid, a.K, lane);
+    load_rows<KT>(t, a.X[0] + s * a.sum_stride, a.ldx, p, valid, a.K, lane);
 #pragma unroll
     for (int T = 0; T < KT; ++T)
 #pragma unroll
       for (int r = 0; r < 4; ++r) in[T][r] += t[T][r];
   }
 
-  // grid.y splits the output chunks over workgroups (more parallelism at small point counts)
-  const int nchunks = a.NO / (16 * OC);
-  int cnt = 0;
-  if ((int)blockIdx.y < nchunks)
-    stage_image(wlds, a.Wp + (long)blockIdx.y * OC * KT * WAVE, chunk_f4(KT, OC), 4, wave, lane);
-  for (int c = blockIdx.y; c < nchunks; c += gridDim.y) {
-    f32x4 acc[OC];
-    init_bias<OC>(acc, a.bias ? a.bias + c * 16 * OC : nullptr, lane);
-    const bool more = c + (int)gridDim.y < nchunks;
-    mm_tiles_pipe<KT, OC>(a.Wp + (long)c * OC * KT * WAVE,
-                          more ? a.Wp + (long)(c + gridDim.y) * OC * KT * WAVE : nullptr, chunk_f4(KT, OC), wlds,
-                          cnt, in, acc, 4, wave, lane);
-    float h[OC][4];
-    acc_to_regs<OC>(acc, h);
-    if (c * 16 * OC < a.nsoft) softmax_heads<OC>(h, a.dh);
-    float* Y = a.Y + c * 16 * OC;
-    if (a.epi == EPI_ACCUM) {
-      float old[OC][4];
-      load_rows<OC>(old, Y, a.ldy, p, valid, 16 * OC, lane);
+  f32x4 acc[OC];
+  init_bias<OC>(acc, a.bias ? a.bias + c * 16 * OC : nullptr, lane);
+  // K-segments: acc += X_s W_s for s < nseg; segment s+1's rows are fetched during segment s's MFMAs
+  for (int sg = 0; sg < a.nseg; ++sg) {
+    const bool more = sg + 1 < a.nseg;
+    float nx[KT][4];
+    auto pre = [&]() {
+      if (more) load_rows<KT>(nx, a.X[sg + 1], a.ldx, p, valid, a.K, lane);
+    };
+    mm_tiles_pipe<KT, OC>(a.Wp[sg] + wchunk, more ? a.Wp[sg + 1] + wchunk : nullptr, chunk_f4(KT, OC), wlds, cnt,
+                          in, acc, 4, wave, lane, pre);
+    if (more) {
 #pragma unroll
-      for (int T = 0; T < OC; ++T)
+      for (int T = 0; T < KT; ++T)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) h[T][r] += old[T][r];
+        for (int r = 0; r < 4; ++r) in[T][r] = nx[T][r];
     }
-    store_rows<OC>(h, Y, a.ldy, p, valid, 16 * OC, lane);
   }
+  float h[OC][4];
+  acc_to_regs<OC>(acc, h);
+  if (c * 16 * OC < a.nsoft) softmax_heads<OC>(h, a.dh);
+  float* Y = a.Y + c * 16 * OC;
+  if (a.epi == EPI_ACCUM) {
+    float old[OC][4];
+    load_rows<OC>(old, Y, a.ldy, p, valid, 16 * OC, lane);
+#pragma unroll
+    for (int T = 0; T < OC; ++T)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) h[T][r] += old[T][r];
+  }
+  store_rows<OC>(h, Y, a.ldy, p, valid, 16 * OC, lane);
+}
+
+template <int D>
+__global__ void __launch_bounds__(256) linear_kernel(LinearArgs a) {
+  __shared__ __attribute__((aligned(16))) float4 wlds[2 * kChunkF4];
+  linear_body<D>(a, wlds);
+}
+
+// several independent projections in one launch: job = blockIdx.z (jobs live in device memory)
+template <int D>
+__global__ void __launch_bounds__(256) linear_batch_kernel(const LinearArgs* __restrict__ jobs) {
+  __shared__ __attribute__((aligned(16))) float4 wlds[2 * kChunkF4];
+  const LinearArgs a = jobs[blockIdx.z];
+  if ((long)blockIdx.x * 64 >= a.P) return;        // whole workgroup: no barrier is skipped unevenly
+  linear_body<D>(a, wlds);
+}
+
+static int linear_nchunks(int D, int NO) {
+  const int oc = lds_och(D / 16, D / 16 < 8 ? D / 16 : 8);   // == linear_body's OC
+  return NO / (16 * oc);
 }
 
 hipError_t launch_linear(const LinearArgs& a, int D, hipStream_t s) {
   if (a.P <= 0) return hipSuccess;
-  const int oc = lds_och(D / 16, D / 16 < 8 ? D / 16 : 8);   // == the kernel's OC
-  const int nchunks = a.NO / (16 * oc);
-  const dim3 grid((a.P + 63) / 64, nchunks), block(256);
+  if (a.nseg < 1 || a.nseg > kMaxSeg) return hipErrorInvalidValue;
+  const dim3 grid((a.P + 63) / 64, linear_nchunks(D, a.NO)), block(256);
   switch (D) {
     case 32: hipLaunchKernelGGL(linear_kernel<32>, grid, block, 0, s, a); break;
     case 48: hipLaunchKernelGGL(linear_kernel<48>, grid, block, 0, s, a); break;
     case 64: hipLaunchKernelGGL(linear_kernel<64>, grid, block, 0, s, a); break;
     case 128: hipLaunchKernelGGL(linear_kernel<128>, grid, block, 0, s, a); break;
     case 256: hipLaunchKernelGGL(linear_kernel<256>, grid, block, 0, s, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_linear_batch(const LinearArgs* jobs_dev, int njobs, int maxP, int NO, int D, hipStream_t s) {
+  if (njobs <= 0 || maxP <= 0) return hipSuccess;
+  const dim3 grid((maxP + 63) / 64, linear_nchunks(D, NO), njobs), block(256);
+  switch (D) {
+    case 32: hipLaunchKernelGGL(linear_batch_kernel<32>, grid, block, 0, s, jobs_dev); break;
+    case 48: hipLaunchKernelGGL(linear_batch_kernel<48>, grid, block, 0, s, jobs_dev); break;
+    case 64: hipLaunchKernelGGL(linear_batch_kernel<64>, grid, block, 0, s, jobs_dev); break;
+    case 128: hipLaunchKernelGGL(linear_batch_kernel<128>, grid, block, 0, s, jobs_dev); break;
+    case 256: hipLaunchKernelGGL(linear_batch_kernel<256>, grid, block, 0, s, jobs_dev); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
