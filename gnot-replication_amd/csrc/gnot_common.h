@@ -191,7 +191,7 @@ GNOT_DEV void mm_tiles_lds(const float4* __restrict__ Wg, float4* lds, const flo
 // landing in the other buffer by LDS-DMA, so the weight stream never stalls the MFMAs at a layer
 // boundary.  One barrier per chunk: it retires chunk i's DMA (the barrier's vmcnt(0)) and frees the
 // buffer chunk i-1 used.  `cnt` counts consumed chunks (buffer parity).
-constexpr int kChunkKB = 32;
+constexpr int kChunkKB = 16;
 constexpr int kChunkF4 = kChunkKB * WAVE;          // float4 per buffer
 
 constexpr int chunk_och(int KT, int OT) {

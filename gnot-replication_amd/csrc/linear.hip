@@ -18,7 +18,7 @@ namespace gnot {
 template <int D>
 GNOT_DEV void linear_body(const LinearArgs& a, float4* wlds) {
   constexpr int KT = D / 16;
-  constexpr int OC = lds_och(KT, (D / 16) < 8 ? (D / 16) : 8);   // output tiles per workgroup chunk
+  constexpr int OC = (D / 16) < 4 ? (D / 16) : 4;   // output tiles per workgroup (grid.y splits NO)
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const long p = ((long)blockIdx.x * 4 + wave) * 16 + (lane & 15);
@@ -89,7 +89,7 @@ __global__ void __launch_bounds__(256) linear_batch_kernel(const LinearArgs* __r
 }
 
 static int linear_nchunks(int D, int NO) {
-  const int oc = lds_och(D / 16, D / 16 < 8 ? D / 16 : 8);   // == linear_body's OC
+  const int oc = (D / 16) < 4 ? (D / 16) : 4;   // == linear_body's OC
   return NO / (16 * oc);
 }
 
