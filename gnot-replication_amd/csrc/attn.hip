@@ -9,10 +9,18 @@
 // un-permuting, so the apply pass WRITES head-major per sample: element (h, n, j) of sample b lands
 // at flat offset off_b*d + (h*N_b + n)*dh + j, and fc_out reads that buffer as plain rows.
 //
-// Kernels here:
-//   attn_apply_fwd / attn_apply_bwd  one 64-point segment per workgroup, one thread per (point, head)
-//                in point-major order (coalesced row reads); every head's (S, z) staged in LDS.
-//   attn_kv_bwd  dK, dV from (dS, dz) per (source point, head), same geometry.
+// Work decomposition (all three kernels): a GROUP of G lanes owns one (point, head) pair; lane q of
+// the group owns C = dh/G consecutive features 4-aligned (G = a power of two, so groups never
+// straddle a wave and their reductions are shfl_xor butterflies).  Consecutive groups are
+// consecutive heads of one point, so a wave's row reads/writes are contiguous.  grid.x = 64-point
+// segment of one sample, grid.y splits the segment's (point, head, lane) tasks into 256-thread
+// workgroups -> ~8x more waves than one thread per (point, head), which is what the chip needs at
+// 10k-point meshes (the per-thread dependent FMA chains were latency-bound).  The (S, z) states are
+// read through the L1/L2 (every group of one head reads the same 1 KiB).
+//
+//   attn_apply_fwd  res (head-major)
+//   attn_apply_bwd  du_i, dden_i per source, d(pre-softmax q)
+//   attn_kv_bwd     d(pre-softmax k), dv from (dS, dz)
 // The cross-point reductions themselves (S, z forward; dS, dz backward) are point-reduction GEMMs
 // on the MFMA path (wgrad.hip, state jobs), one job per sample.
 #include "gnot_common.h"
@@ -20,215 +28,224 @@
 
 namespace gnot {
 
-// u = x M  for a row vector x[DH] and a row-major DH x DH matrix M in LDS (float4 row reads)
+// lanes per (point, head) for head width DH
+constexpr int head_lanes(int q4) {   // largest power of two <= 16 dividing q4 = DH / 4
+  int g = 16;
+  while (g > 1 && q4 % g != 0) g >>= 1;
+  return g;
+}
+
 template <int DH>
-GNOT_DEV void rowvec_times_mat(const float (&x)[DH], const float* M, float (&u)[DH]) {
+struct HeadSplit {
+  static constexpr int G = head_lanes(DH / 4);
+  static constexpr int C = DH / G;          // features owned per lane (multiple of 4)
+  static_assert(C % 4 == 0 && C * G == DH, "head width must split into 4-aligned lane slices");
+};
+
+template <int G>
+GNOT_DEV float group_sum(float v) {
 #pragma unroll
-  for (int j = 0; j < DH; ++j) u[j] = 0.f;
+  for (int m = 1; m < G; m <<= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+
+template <int N>
+GNOT_DEV void load_vec(float (&dst)[N], const float* __restrict__ src) {
 #pragma unroll
-  for (int k = 0; k < DH; ++k) {
-#pragma unroll
-    for (int j = 0; j < DH; j += 4) {
-      const float4 m = *reinterpret_cast<const float4*>(M + k * DH + j);
-      u[j] = fmaf(x[k], m.x, u[j]);
-      u[j + 1] = fmaf(x[k], m.y, u[j + 1]);
-      u[j + 2] = fmaf(x[k], m.z, u[j + 2]);
-      u[j + 3] = fmaf(x[k], m.w, u[j + 3]);
-    }
+  for (int j = 0; j < N; j += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(src + j);
+    dst[j] = v.x; dst[j + 1] = v.y; dst[j + 2] = v.z; dst[j + 3] = v.w;
   }
 }
 
-// x . row  for a row of DH floats in LDS
-template <int DH>
-GNOT_DEV float dot_row(const float (&x)[DH], const float* row) {
-  float a = 0.f, b = 0.f;
+template <int N>
+GNOT_DEV void store_vec(float* __restrict__ dst, const float (&v)[N]) {
 #pragma unroll
-  for (int j = 0; j < DH; j += 4) {
-    const float4 m = *reinterpret_cast<const float4*>(row + j);
-    a = fmaf(x[j], m.x, a);
-    b = fmaf(x[j + 1], m.y, b);
-    a = fmaf(x[j + 2], m.z, a);
-    b = fmaf(x[j + 3], m.w, b);
-  }
-  return a + b;
+  for (int j = 0; j < N; j += 4) *reinterpret_cast<float4*>(dst + j) = make_float4(v[j], v[j + 1], v[j + 2], v[j + 3]);
+}
+
+// task decode: returns false for tasks past the segment's end (whole groups, so shuffles stay in-group)
+struct Task {
+  long n;      // global (packed) point index
+  int h;       // head
+  int q;       // lane within the group
+};
+
+template <int G>
+GNOT_DEV bool decode_task(const int4& ch, int H, Task& t) {
+  const int idx = blockIdx.y * 256 + threadIdx.x;
+  const int grp = idx / G;
+  if (grp >= ch.z * H) return false;
+  t.q = idx % G;
+  t.n = ch.y + grp / H;
+  t.h = grp % H;
+  return true;
 }
 
 // ---------------------------------------------------------------- apply (forward)
 template <int DH>
 __global__ void __launch_bounds__(256) attn_apply_fwd_kernel(AttnApplyArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int4 ch = a.chunks[blockIdx.x];
-  const int b = ch.x;
-  const int H = a.H;
+  constexpr int G = HeadSplit<DH>::G, C = HeadSplit<DH>::C;
   constexpr int ph = DH * DH + DH;
-  const int per = H * ph;
-  for (int i = threadIdx.x; i < a.nsrc * per; i += 256) {
-    const int sidx = i / per, e = i % per;
-    smem[i] = a.state[sidx][(long)b * per + e];
-  }
-  __syncthreads();
+  const int4 ch = a.chunks[blockIdx.x];
+  Task t;
+  if (!decode_task<G>(ch, a.H, t)) return;
+  const int b = ch.x;
   const long off_b = a.off[b];
   const long Nb = a.off[b + 1] - off_b;
-  const int d = H * DH;
-  const float inv_nsrc = 1.0f / (float)a.nsrc;
-  // point-major work order: consecutive lanes read consecutive heads of one point row (coalesced)
-  for (int idx = threadIdx.x; idx < ch.z * H; idx += 256) {
-    const long n = ch.y + idx / H;       // global point index
-    const int h = idx % H;
-    float q[DH], os[DH];
+  const int c0 = t.q * C;
+  float qf[DH];
+  load_vec<DH>(qf, a.q + t.n * a.ldq + t.h * DH);
+  float os[C];
 #pragma unroll
-    for (int j = 0; j < DH; j += 4) {
-      const float4 v = *reinterpret_cast<const float4*>(a.q + n * a.ldq + h * DH + j);
-      q[j] = v.x; q[j + 1] = v.y; q[j + 2] = v.z; q[j + 3] = v.w;
+  for (int c = 0; c < C; ++c) os[c] = 0.f;
+  for (int s = 0; s < a.nsrc; ++s) {
+    const float* S = a.state[s] + (long)b * a.H * ph + t.h * ph;
+    const float* z = S + DH * DH;
+    float den = 0.f, u[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) u[c] = 0.f;
+#pragma unroll
+    for (int k = 0; k < DH; ++k) {
+      den = fmaf(qf[k], z[k], den);
+      float srow[C];
+      load_vec<C>(srow, S + k * DH + c0);
+#pragma unroll
+      for (int c = 0; c < C; ++c) u[c] = fmaf(qf[k], srow[c], u[c]);
     }
+    const float inv = 1.0f / den;
 #pragma unroll
-    for (int j = 0; j < DH; ++j) os[j] = 0.f;
-    for (int sidx = 0; sidx < a.nsrc; ++sidx) {
-      const float* S = smem + sidx * per + h * ph;
-      const float* z = S + DH * DH;
-      float den = 0.f;
-#pragma unroll
-      for (int k = 0; k < DH; ++k) den = fmaf(q[k], z[k], den);
-      float u[DH];
-      rowvec_times_mat<DH>(q, S, u);
-      const float inv = 1.0f / den;
-#pragma unroll
-      for (int j = 0; j < DH; ++j) os[j] = fmaf(u[j], inv, os[j]);
-    }
-    float* dst = a.res + off_b * d + ((long)h * Nb + (n - off_b)) * DH;
-#pragma unroll
-    for (int j = 0; j < DH; j += 4)
-      *reinterpret_cast<float4*>(dst + j) =
-          make_float4(q[j] + os[j] * inv_nsrc, q[j + 1] + os[j + 1] * inv_nsrc,
-                      q[j + 2] + os[j + 2] * inv_nsrc, q[j + 3] + os[j + 3] * inv_nsrc);
+    for (int c = 0; c < C; ++c) os[c] = fmaf(u[c], inv, os[c]);
   }
+  const float inv_nsrc = 1.0f / (float)a.nsrc;
+  float r[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) r[c] = fmaf(os[c], inv_nsrc, qf[c0 + c]);
+  store_vec<C>(a.res + off_b * (long)a.H * DH + ((long)t.h * Nb + (t.n - off_b)) * DH + c0, r);
 }
 
 // ---------------------------------------------------------------- apply (backward)
+// dO = dres/nsrc; per source: o = u/den, du = dO/den, dden = -(dO.u)/den^2, dq += du S^T + dden z;
+// dq starts at dres (the q residual); finally the feature-softmax backward of q.
 template <int DH>
 __global__ void __launch_bounds__(256) attn_apply_bwd_kernel(AttnApplyArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int4 ch = a.chunks[blockIdx.x];
-  const int b = ch.x;
-  const int H = a.H;
+  constexpr int G = HeadSplit<DH>::G, C = HeadSplit<DH>::C;
   constexpr int ph = DH * DH + DH;
-  const int per = H * ph;
-  for (int i = threadIdx.x; i < a.nsrc * per; i += 256) {
-    const int sidx = i / per, e = i % per;
-    smem[i] = a.state[sidx][(long)b * per + e];
-  }
-  __syncthreads();
+  const int4 ch = a.chunks[blockIdx.x];
+  Task t;
+  if (!decode_task<G>(ch, a.H, t)) return;
+  const int b = ch.x;
   const long off_b = a.off[b];
   const long Nb = a.off[b + 1] - off_b;
-  const int d = H * DH;
+  const int c0 = t.q * C;
   const float inv_nsrc = 1.0f / (float)a.nsrc;
-  for (int idx = threadIdx.x; idx < ch.z * H; idx += 256) {
-    const long n = ch.y + idx / H;
-    const int h = idx % H;
-    float q[DH], dO[DH], dq[DH];
-    const float* src = a.dres + off_b * d + ((long)h * Nb + (n - off_b)) * DH;
+  float qf[DH], dOf[DH];
+  load_vec<DH>(qf, a.q + t.n * a.ldq + t.h * DH);
+  load_vec<DH>(dOf, a.dres + off_b * (long)a.H * DH + ((long)t.h * Nb + (t.n - off_b)) * DH);
+  float dq[C];
 #pragma unroll
-    for (int j = 0; j < DH; j += 4) {
-      const float4 v = *reinterpret_cast<const float4*>(a.q + n * a.ldq + h * DH + j);
-      q[j] = v.x; q[j + 1] = v.y; q[j + 2] = v.z; q[j + 3] = v.w;
-      const float4 g = *reinterpret_cast<const float4*>(src + j);
-      dq[j] = g.x; dq[j + 1] = g.y; dq[j + 2] = g.z; dq[j + 3] = g.w;
+  for (int c = 0; c < C; ++c) dq[c] = dOf[c0 + c];
+#pragma unroll
+  for (int j = 0; j < DH; ++j) dOf[j] *= inv_nsrc;
+  for (int s = 0; s < a.nsrc; ++s) {
+    const float* S = a.state[s] + (long)b * a.H * ph + t.h * ph;
+    const float* z = S + DH * DH;
+    float den = 0.f, u[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) u[c] = 0.f;
+#pragma unroll
+    for (int k = 0; k < DH; ++k) {
+      den = fmaf(qf[k], z[k], den);
+      float srow[C];
+      load_vec<C>(srow, S + k * DH + c0);
+#pragma unroll
+      for (int c = 0; c < C; ++c) u[c] = fmaf(qf[k], srow[c], u[c]);
     }
+    float dot = 0.f;
 #pragma unroll
-    for (int j = 0; j < DH; ++j) dO[j] = dq[j] * inv_nsrc;
-    for (int sidx = 0; sidx < a.nsrc; ++sidx) {
-      const float* S = smem + sidx * per + h * ph;
-      const float* z = S + DH * DH;
-      float den = 0.f;
+    for (int c = 0; c < C; ++c) dot = fmaf(dOf[c0 + c], u[c], dot);
+    dot = group_sum<G>(dot);
+    const float inv = 1.0f / den;
+    const float dden = -dot * inv * inv;
+    float du[C];
 #pragma unroll
-      for (int k = 0; k < DH; ++k) den = fmaf(q[k], z[k], den);
-      float u[DH];
-      rowvec_times_mat<DH>(q, S, u);
-      const float inv = 1.0f / den;
-      // o = u/den ; du = dO/den ; dden = -(dO . o)/den
-      float dot = 0.f;
+    for (int c = 0; c < C; ++c) du[c] = dOf[c0 + c] * inv;
+    store_vec<C>(a.du[s] + t.n * a.lddu + t.h * DH + c0, du);
+    if (t.q == 0) a.dden[s][t.n * a.H + t.h] = dden;
+    // dq[k] += sum_j du_j S[k][j] + dden z[k] for this lane's rows k = c0 .. c0+C-1 (du = dO * inv)
 #pragma unroll
-      for (int j = 0; j < DH; ++j) dot = fmaf(dO[j], u[j], dot);
-      const float dden = -dot * inv * inv;
-      float du[DH];
+    for (int c = 0; c < C; ++c) {
+      float srow[DH];
+      load_vec<DH>(srow, S + (c0 + c) * DH);
+      float acc = 0.f;
 #pragma unroll
-      for (int j = 0; j < DH; ++j) du[j] = dO[j] * inv;
-      // dq += du S^T + dden z
-#pragma unroll
-      for (int k = 0; k < DH; ++k) dq[k] = fmaf(dden, z[k], dq[k] + dot_row<DH>(du, S + k * DH));
-      float* dup = a.du[sidx] + n * a.lddu + h * DH;
-#pragma unroll
-      for (int j = 0; j < DH; j += 4)
-        *reinterpret_cast<float4*>(dup + j) = make_float4(du[j], du[j + 1], du[j + 2], du[j + 3]);
-      a.dden[sidx][n * H + h] = dden;
+      for (int j = 0; j < DH; ++j) acc = fmaf(dOf[j], srow[j], acc);
+      dq[c] = fmaf(acc, inv, fmaf(dden, z[c0 + c], dq[c]));
     }
-    // softmax backward over the head's features
-    float qdq = 0.f;
-#pragma unroll
-    for (int j = 0; j < DH; ++j) qdq = fmaf(q[j], dq[j], qdq);
-    float* dst = a.dq_pre + n * a.lddq + h * DH;
-#pragma unroll
-    for (int j = 0; j < DH; j += 4)
-      *reinterpret_cast<float4*>(dst + j) =
-          make_float4(q[j] * (dq[j] - qdq), q[j + 1] * (dq[j + 1] - qdq), q[j + 2] * (dq[j + 2] - qdq),
-                      q[j + 3] * (dq[j + 3] - qdq));
   }
+  float qdq = 0.f;
+#pragma unroll
+  for (int c = 0; c < C; ++c) qdq = fmaf(qf[c0 + c], dq[c], qdq);
+  qdq = group_sum<G>(qdq);
+  float dpre[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) dpre[c] = qf[c0 + c] * (dq[c] - qdq);
+  store_vec<C>(a.dq_pre + t.n * a.lddq + t.h * DH + c0, dpre);
 }
 
 // ---------------------------------------------------------------- K/V backward
+// dk = dz + v dS^T, dv = k dS (per head), then the feature-softmax backward of k.
 template <int DH>
-GNOT_DEV void attn_kv_bwd_body(const AttnKVBwdArgs& a, float* smem) {
-  const int4 ch = a.chunks[blockIdx.x];
-  const int b = ch.x;
-  const int H = a.H;
+GNOT_DEV void attn_kv_bwd_body(const AttnKVBwdArgs& a, const int4& ch) {
+  constexpr int G = HeadSplit<DH>::G, C = HeadSplit<DH>::C;
   constexpr int ph = DH * DH + DH;
-  const int per = H * ph;
-  for (int i = threadIdx.x; i < per; i += 256) smem[i] = a.dstate[(long)b * per + i];
-  __syncthreads();
-  for (int idx = threadIdx.x; idx < ch.z * H; idx += 256) {
-    const long m = ch.y + idx / H;
-    const int h = idx % H;
-    const float* dS = smem + h * ph;
-    const float* dz = dS + DH * DH;
-    float k[DH], v[DH];
+  Task t;
+  if (!decode_task<G>(ch, a.H, t)) return;
+  const int b = ch.x;
+  const int c0 = t.q * C;
+  const float* dS = a.dstate + (long)b * a.H * ph + t.h * ph;
+  const float* dz = dS + DH * DH;
+  float kf[DH], vf[DH];
+  load_vec<DH>(kf, a.k + t.n * a.ldkv + t.h * DH);
+  load_vec<DH>(vf, a.v + t.n * a.ldkv + t.h * DH);
+  float dk[C], dv[C];
 #pragma unroll
-    for (int j = 0; j < DH; j += 4) {
-      const float4 kv = *reinterpret_cast<const float4*>(a.k + m * a.ldkv + h * DH + j);
-      k[j] = kv.x; k[j + 1] = kv.y; k[j + 2] = kv.z; k[j + 3] = kv.w;
-      const float4 vv = *reinterpret_cast<const float4*>(a.v + m * a.ldkv + h * DH + j);
-      v[j] = vv.x; v[j + 1] = vv.y; v[j + 2] = vv.z; v[j + 3] = vv.w;
-    }
-    float dk[DH], dv[DH];
+  for (int c = 0; c < C; ++c) {
+    float srow[DH];
+    load_vec<DH>(srow, dS + (c0 + c) * DH);
+    float acc = dz[c0 + c];
 #pragma unroll
-    for (int i = 0; i < DH; ++i) dk[i] = dz[i] + dot_row<DH>(v, dS + i * DH);
-    rowvec_times_mat<DH>(k, dS, dv);
-    float kdk = 0.f;
-#pragma unroll
-    for (int i = 0; i < DH; ++i) kdk = fmaf(k[i], dk[i], kdk);
-    float* dkp = a.dk + m * a.lddkv + h * DH;
-    float* dvp = a.dv + m * a.lddkv + h * DH;
-#pragma unroll
-    for (int j = 0; j < DH; j += 4) {
-      *reinterpret_cast<float4*>(dkp + j) =
-          make_float4(k[j] * (dk[j] - kdk), k[j + 1] * (dk[j + 1] - kdk), k[j + 2] * (dk[j + 2] - kdk),
-                      k[j + 3] * (dk[j + 3] - kdk));
-      *reinterpret_cast<float4*>(dvp + j) = make_float4(dv[j], dv[j + 1], dv[j + 2], dv[j + 3]);
-    }
+    for (int j = 0; j < DH; ++j) acc = fmaf(vf[j], srow[j], acc);
+    dk[c] = acc;
+    dv[c] = 0.f;
   }
+#pragma unroll
+  for (int i = 0; i < DH; ++i) {
+    float srow[C];
+    load_vec<C>(srow, dS + i * DH + c0);
+#pragma unroll
+    for (int c = 0; c < C; ++c) dv[c] = fmaf(kf[i], srow[c], dv[c]);
+  }
+  float kdk = 0.f;
+#pragma unroll
+  for (int c = 0; c < C; ++c) kdk = fmaf(kf[c0 + c], dk[c], kdk);
+  kdk = group_sum<G>(kdk);
+#pragma unroll
+  for (int c = 0; c < C; ++c) dk[c] = kf[c0 + c] * (dk[c] - kdk);
+  store_vec<C>(a.dk + t.n * a.lddkv + t.h * DH + c0, dk);
+  store_vec<C>(a.dv + t.n * a.lddkv + t.h * DH + c0, dv);
 }
 
 template <int DH>
 __global__ void __launch_bounds__(256) attn_kv_bwd_kernel(AttnKVBwdArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  attn_kv_bwd_body<DH>(a, smem);
+  attn_kv_bwd_body<DH>(a, a.chunks[blockIdx.x]);
 }
 
 template <int DH>
 __global__ void __launch_bounds__(256) attn_kv_bwd_batch_kernel(const AttnKVBwdArgs* __restrict__ jobs) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const AttnKVBwdArgs a = jobs[blockIdx.y];
+  const AttnKVBwdArgs& a = jobs[blockIdx.z];
   if ((int)blockIdx.x >= a.nchunks) return;
-  attn_kv_bwd_body<DH>(a, smem);
+  attn_kv_bwd_body<DH>(a, a.chunks[blockIdx.x]);
 }
 
 #define GNOT_DH_SWITCH(DHV, ...)        \
@@ -242,43 +259,38 @@ __global__ void __launch_bounds__(256) attn_kv_bwd_batch_kernel(const AttnKVBwdA
     default: return hipErrorInvalidValue;                    \
   }
 
-template <typename K>
-static void allow_lds(K kernel, size_t bytes) {
-  if (bytes > 64 * 1024)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+// workgroups per 64-point segment: ceil(64 * H * G / 256)
+template <int DH>
+static unsigned seg_split(int H) {
+  return (unsigned)((64 * H * HeadSplit<DH>::G + 255) / 256);
 }
 
 hipError_t launch_attn_apply_fwd(const AttnApplyArgs& a, hipStream_t s) {
   if (a.nchunks <= 0) return hipSuccess;
-  const size_t lds = (size_t)a.nsrc * a.H * (a.dh * a.dh + a.dh) * sizeof(float);
-  GNOT_DH_SWITCH(a.dh, allow_lds(attn_apply_fwd_kernel<DH>, lds);
-                 hipLaunchKernelGGL(attn_apply_fwd_kernel<DH>, dim3(a.nchunks), dim3(256), lds, s, a));
+  GNOT_DH_SWITCH(a.dh, hipLaunchKernelGGL(attn_apply_fwd_kernel<DH>, dim3(a.nchunks, seg_split<DH>(a.H)), dim3(256),
+                                          0, s, a));
   return hipGetLastError();
 }
 
 hipError_t launch_attn_apply_bwd(const AttnApplyArgs& a, hipStream_t s) {
   if (a.nchunks <= 0) return hipSuccess;
-  const size_t lds = (size_t)a.nsrc * a.H * (a.dh * a.dh + a.dh) * sizeof(float);
-  GNOT_DH_SWITCH(a.dh, allow_lds(attn_apply_bwd_kernel<DH>, lds);
-                 hipLaunchKernelGGL(attn_apply_bwd_kernel<DH>, dim3(a.nchunks), dim3(256), lds, s, a));
+  GNOT_DH_SWITCH(a.dh, hipLaunchKernelGGL(attn_apply_bwd_kernel<DH>, dim3(a.nchunks, seg_split<DH>(a.H)), dim3(256),
+                                          0, s, a));
   return hipGetLastError();
 }
 
 hipError_t launch_attn_kv_bwd(const AttnKVBwdArgs& a, hipStream_t s) {
   if (a.nchunks <= 0) return hipSuccess;
-  const size_t lds = (size_t)a.H * (a.dh * a.dh + a.dh) * sizeof(float);
-  GNOT_DH_SWITCH(a.dh, allow_lds(attn_kv_bwd_kernel<DH>, lds);
-                 hipLaunchKernelGGL(attn_kv_bwd_kernel<DH>, dim3(a.nchunks), dim3(256), lds, s, a));
+  GNOT_DH_SWITCH(a.dh, hipLaunchKernelGGL(attn_kv_bwd_kernel<DH>, dim3(a.nchunks, seg_split<DH>(a.H)), dim3(256), 0,
+                                          s, a));
   return hipGetLastError();
 }
 
 hipError_t launch_attn_kv_bwd_batch(const AttnKVBwdArgs* jobs_dev, int njobs, int maxchunks, int H, int dh,
                                     hipStream_t s) {
   if (njobs <= 0 || maxchunks <= 0) return hipSuccess;
-  const size_t lds = (size_t)H * (dh * dh + dh) * sizeof(float);
-  GNOT_DH_SWITCH(dh, allow_lds(attn_kv_bwd_batch_kernel<DH>, lds);
-                 hipLaunchKernelGGL(attn_kv_bwd_batch_kernel<DH>, dim3(maxchunks, njobs), dim3(256), lds, s, jobs_dev));
+  GNOT_DH_SWITCH(dh, hipLaunchKernelGGL(attn_kv_bwd_batch_kernel<DH>, dim3(maxchunks, seg_split<DH>(H), njobs),
+                                        dim3(256), 0, s, jobs_dev));
   return hipGetLastError();
 }
 

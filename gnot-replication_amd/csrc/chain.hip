@@ -17,12 +17,17 @@
 
 namespace gnot {
 
+// waves (16 points each) per workgroup; the workgroup shares one LDS weight stream.  Two waves give
+// ~5 workgroups per CU at 10k-point meshes instead of 2-3 (less tail imbalance, better MFMA fill)
+// for twice the L2->LDS weight traffic.
+constexpr int kChainWaves = 4;
+
 template <int D, int KT0, int OTL>
-__global__ void __launch_bounds__(256) chain_fwd_kernel(ChainArgs a) {
+__global__ void __launch_bounds__(64 * kChainWaves) chain_fwd_kernel(ChainArgs a) {
   constexpr int DT = D / 16;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const long p = ((long)blockIdx.x * 4 + wave) * 16 + (lane & 15);
+  const long p = ((long)blockIdx.x * kChainWaves + wave) * 16 + (lane & 15);
   const bool valid = p < a.P;
   const int e = blockIdx.y;
   const int nl = a.nlin;
@@ -31,7 +36,7 @@ __global__ void __launch_bounds__(256) chain_fwd_kernel(ChainArgs a) {
   __shared__ __attribute__((aligned(16))) float4 wlds[2 * kChunkF4];
   int cnt = 0;
   // the weight stream: layer 0 | hidden layers | last layer, one chunk always in flight
-  stage_image(wlds, L[0].Wp, chunk_f4(KT0, DT), 4, wave, lane);
+  stage_image(wlds, L[0].Wp, chunk_f4(KT0, DT), kChainWaves, wave, lane);
   auto next_f4 = [&](int l) { return (l == nl - 1) ? chunk_f4(DT, OTL) : chunk_f4(DT, DT); };
 
   float h[DT][4];
@@ -40,7 +45,7 @@ __global__ void __launch_bounds__(256) chain_fwd_kernel(ChainArgs a) {
     load_rows<KT0>(x0, a.X, a.ldx, p, valid, a.in_dim, lane);
     f32x4 acc[DT];
     init_bias<DT>(acc, L[0].bias, lane);
-    mm_tiles_pipe<KT0, DT>(L[0].Wp, L[1].Wp, next_f4(1), wlds, cnt, x0, acc, 4, wave, lane);
+    mm_tiles_pipe<KT0, DT>(L[0].Wp, L[1].Wp, next_f4(1), wlds, cnt, x0, acc, kChainWaves, wave, lane);
     acc_to_regs<DT>(acc, h);
   }
   if (save) store_rows<DT>(h, save, D, p, valid, D, lane);
@@ -52,7 +57,7 @@ __global__ void __launch_bounds__(256) chain_fwd_kernel(ChainArgs a) {
   for (int l = 1; l < nl - 1; ++l) {
     f32x4 acc[DT];
     init_bias<DT>(acc, L[l].bias, lane);
-    mm_tiles_pipe<DT, DT>(L[l].Wp, L[l + 1].Wp, next_f4(l + 1), wlds, cnt, h, acc, 4, wave, lane);
+    mm_tiles_pipe<DT, DT>(L[l].Wp, L[l + 1].Wp, next_f4(l + 1), wlds, cnt, h, acc, kChainWaves, wave, lane);
     acc_to_regs<DT>(acc, h);
     if (save) store_rows<DT>(h, save + l * a.save_layer_stride, D, p, valid, D, lane);
 #pragma unroll
@@ -65,7 +70,7 @@ __global__ void __launch_bounds__(256) chain_fwd_kernel(ChainArgs a) {
   {
     f32x4 acc[OTL];
     init_bias<OTL>(acc, L[nl - 1].bias, lane);
-    mm_tiles_pipe<DT, OTL>(L[nl - 1].Wp, nullptr, 0, wlds, cnt, h, acc, 4, wave, lane);
+    mm_tiles_pipe<DT, OTL>(L[nl - 1].Wp, nullptr, 0, wlds, cnt, h, acc, kChainWaves, wave, lane);
     acc_to_regs<OTL>(acc, y);
   }
   if (save) store_rows<OTL>(y, save + (nl - 1) * a.save_layer_stride, D, p, valid, 16 * OTL, lane);
@@ -111,12 +116,12 @@ __global__ void __launch_bounds__(256) chain_fwd_kernel(ChainArgs a) {
 }
 
 template <int D, int KT0, int OTL>
-__global__ void __launch_bounds__(256) chain_bwd_kernel(ChainArgs a) {
+__global__ void __launch_bounds__(64 * kChainWaves) chain_bwd_kernel(ChainArgs a) {
   constexpr int DT = D / 16;
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4;
   const int wave = threadIdx.x >> 6;
-  const long p = ((long)blockIdx.x * 4 + wave) * 16 + (lane & 15);
+  const long p = ((long)blockIdx.x * kChainWaves + wave) * 16 + (lane & 15);
   const bool valid = p < a.P;
   const int e = blockIdx.y;
   const int nl = a.nlin;
@@ -126,7 +131,7 @@ __global__ void __launch_bounds__(256) chain_bwd_kernel(ChainArgs a) {
   __shared__ __attribute__((aligned(16))) float4 wlds[2 * kChunkF4];
   int cnt = 0;
   // transposed-weight stream in reverse layer order: last | hidden (nl-2 .. 1) | first (if dX)
-  stage_image(wlds, L[nl - 1].WpT, chunk_f4(OTL, DT), 4, wave, lane);
+  stage_image(wlds, L[nl - 1].WpT, chunk_f4(OTL, DT), kChainWaves, wave, lane);
   auto next_W = [&](int l) -> const float4* {      // the layer processed after layer l
     if (l - 1 >= 1) return L[l - 1].WpT;
     return a.dX ? L[0].WpT : nullptr;
@@ -181,7 +186,7 @@ __global__ void __launch_bounds__(256) chain_bwd_kernel(ChainArgs a) {
     f32x4 acc[DT];
     init_bias<DT>(acc, nullptr, lane);
     auto pre = [&]() { load_rows<DT>(hs, save + (nl - 2) * a.save_layer_stride, D, p, valid, D, lane); };
-    mm_tiles_pipe<OTL, DT>(L[nl - 1].WpT, next_W(nl - 1), next_f4(nl - 1), wlds, cnt, dy, acc, 4, wave, lane,
+    mm_tiles_pipe<OTL, DT>(L[nl - 1].WpT, next_W(nl - 1), next_f4(nl - 1), wlds, cnt, dy, acc, kChainWaves, wave, lane,
                            pre);
     acc_to_regs<DT>(acc, gr);
   }
@@ -195,7 +200,7 @@ __global__ void __launch_bounds__(256) chain_bwd_kernel(ChainArgs a) {
     f32x4 acc[DT];
     init_bias<DT>(acc, nullptr, lane);
     auto pre = [&]() { load_rows<DT>(hs, save + (l - 1) * a.save_layer_stride, D, p, valid, D, lane); };
-    mm_tiles_pipe<DT, DT>(L[l].WpT, next_W(l), next_f4(l), wlds, cnt, gr, acc, 4, wave, lane, pre);
+    mm_tiles_pipe<DT, DT>(L[l].WpT, next_W(l), next_f4(l), wlds, cnt, gr, acc, kChainWaves, wave, lane, pre);
     acc_to_regs<DT>(acc, gr);
   }
   // ---- first Linear (hs now holds the saved pre-activation of Linear 0)
@@ -207,7 +212,7 @@ __global__ void __launch_bounds__(256) chain_bwd_kernel(ChainArgs a) {
   if (a.dX) {
     f32x4 acc[KT0];
     init_bias<KT0>(acc, nullptr, lane);
-    mm_tiles_pipe<DT, KT0>(L[0].WpT, nullptr, 0, wlds, cnt, gr, acc, 4, wave, lane);
+    mm_tiles_pipe<DT, KT0>(L[0].WpT, nullptr, 0, wlds, cnt, gr, acc, kChainWaves, wave, lane);
     float dx[KT0][4];
     acc_to_regs<KT0>(acc, dx);
     store_rows<KT0>(dx, a.dX + e * a.dx_chain_stride, a.lddx, p, valid, a.in_dim, lane);
@@ -217,7 +222,7 @@ __global__ void __launch_bounds__(256) chain_bwd_kernel(ChainArgs a) {
 template <int D>
 static hipError_t launch_chain_d(const ChainArgs& a, bool bwd, hipStream_t s) {
   constexpr int DT = D / 16;
-  const dim3 grid((a.P + 63) / 64, a.nchains), block(256);
+  const dim3 grid((a.P + 16 * kChainWaves - 1) / (16 * kChainWaves), a.nchains), block(64 * kChainWaves);
 #define GNOT_CHAIN_CASE(K0, OL)                                                              \
   if (a.KT0 == K0 && a.OTL == OL) {                                                           \
     if (bwd) hipLaunchKernelGGL((chain_bwd_kernel<D, K0, OL>), grid, block, 0, s, a);          \

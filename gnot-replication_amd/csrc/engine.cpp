@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -448,13 +449,14 @@ static void finish_group(gnot_plan* p, WgradGroup& G) {
     J.tiles_i = (J.in + kPTile - 1) / kPTile;
     tiles += J.diag_only ? J.tiles_o : J.tiles_o * J.tiles_i;
   }
-  const long want = std::max<long>(1, (kTargetWGs + std::max<long>(tiles, 1) - 1) / std::max<long>(tiles, 1));
+  // floor, not ceil: never more than kTargetWGs (= 2 per CU) workgroups, so no CU runs a third one
+  const long want = std::max<long>(1, kTargetWGs / std::max<long>(tiles, 1));
   G.wg_prefix.clear();
   G.red_prefix.clear();
   G.slab_floats = 0;
   int wg = 0, red = 0;
   for (auto& J : G.jobs) {
-    const long minpts = J.state_dh > 0 ? 32 : kMinSplitPoints;   // state reductions: tiny, latency-bound
+    const long minpts = kMinSplitPoints;   // >= 4 LDS stages per workgroup: bounds the split-K slab traffic
     const long maxs = std::max<long>(1, (J.P + minpts - 1) / minpts);
     J.splits = (int)std::min<long>(std::min<long>(want, maxs), 256);
     const int nt = J.diag_only ? J.tiles_o : J.tiles_o * J.tiles_i;
@@ -469,6 +471,27 @@ static void finish_group(gnot_plan* p, WgradGroup& G) {
   G.total_red = red;
   size_t& slab = (!G.jobs.empty() && G.jobs[0].state_dh > 0) ? p->slab_state_floats : p->slab_wgrad_floats;
   slab = std::max(slab, G.slab_floats);
+}
+
+// attention-state group (state.hip): one job per sample, ceil(P / kStatePts) partial states each
+static void finish_state_group(gnot_plan* p, WgradGroup& G) {
+  G.wg_prefix.clear();
+  G.red_prefix.clear();
+  G.slab_floats = 0;
+  int wg = 0, red = 0;
+  for (auto& J : G.jobs) {
+    const int per = J.out / J.state_dh * (J.state_dh * J.state_dh + J.state_dh);
+    J.splits = std::max(1, (J.P + state_pts(J.out) - 1) / state_pts(J.out));
+    J.slab_off = (long)G.slab_floats;
+    G.slab_floats += (size_t)J.splits * per;
+    G.wg_prefix.push_back(wg);
+    wg += J.splits;
+    G.red_prefix.push_back(red);
+    red += per;
+  }
+  G.total_wgs = wg;
+  G.total_red = red;
+  p->slab_state_floats = std::max(p->slab_state_floats, G.slab_floats);
 }
 
 template <typename F>
@@ -544,7 +567,7 @@ static void build_groups(gnot_plan* p) {
       J.P = (int)(off[b + 1] - off[b]);
       G.jobs.push_back(J);
     }
-    finish_group(p, G);
+    finish_state_group(p, G);
   };
 
   for (int l = 0; l < p->L; ++l) {
@@ -588,7 +611,7 @@ static void build_groups(gnot_plan* p) {
           p->st_fn.jobs.push_back(J);
         }
       }
-    finish_group(p, p->st_fn);
+    finish_state_group(p, p->st_fn);
   }
   if (!tr) return;
 
@@ -1082,7 +1105,7 @@ double group_flops(const WgradGroup& G) {
 int run_state(Ctx& c, const WgradGroup& G) {
   if (G.jobs.empty()) return GNOT_OK;
   ProfScope ps(c, "state", group_flops(G));
-  GNOT_CK(launch_wgrad(G.d_jobs, G.d_wg_prefix, (int)G.jobs.size(), G.total_wgs, G.d_red_prefix,
+  GNOT_CK(launch_state(G.d_jobs, G.d_wg_prefix, (int)G.jobs.size(), G.total_wgs, G.d_red_prefix,
                        G.total_red, c.p->P_("slab_state"), c.s));
   return GNOT_OK;
 }
@@ -1108,6 +1131,13 @@ int guard_write(Ctx& c, const float* buf) {
 int run_wgrad_side(Ctx& c, const WgradGroup& G, std::initializer_list<const float*> reads) {
   if (G.jobs.empty()) return GNOT_OK;
   gnot_plan* p = c.p;
+  static const bool serial = std::getenv("GNOT_SERIAL_WGRAD") != nullptr;   // diagnostics: no overlap
+  if (serial) {
+    ProfScope ps(c, "wgrad", group_flops(G));
+    GNOT_CK(launch_wgrad(G.d_jobs, G.d_wg_prefix, (int)G.jobs.size(), G.total_wgs, G.d_red_prefix,
+                         G.total_red, p->P_("slab_wgrad"), c.s));
+    return GNOT_OK;
+  }
   hipEvent_t fork = next_event(p);
   GNOT_CK(hipEventRecord(fork, c.s));
   GNOT_CK(hipStreamWaitEvent(p->side, fork, 0));

@@ -102,6 +102,14 @@ struct WgradJob {
 hipError_t launch_wgrad(const WgradJob* jobs_dev, const int* wg_prefix_dev, int njobs, int total_wgs,
                         const int* red_prefix_dev, int total_red, float* slab, hipStream_t s);
 
+// ------------------------------------------------------------------ attention states (state.hip)
+// Jobs are WgradJobs with state_dh > 0: A = dz/lddz, B = x/ldx, optional w/ldw, out = dW as
+// [H][dh*dh + dh], `splits` partials of state_pts(d) points each at slab + slab_off.
+// points per partial state: the workgroup's A and B rows fill <= 32 KiB of LDS each
+inline __host__ __device__ int state_pts(int d) { return d <= 128 ? 64 : 8192 / d; }
+hipError_t launch_state(const WgradJob* jobs_dev, const int* wg_prefix_dev, int njobs, int total_wgs,
+                        const int* red_prefix_dev, int total_red, float* slab, hipStream_t s);
+
 // ------------------------------------------------------------------ attention (attn.hip)
 struct AttnApplyArgs {
   const float* q; long ldq;          // post-softmax q, point-major
