@@ -37,6 +37,17 @@ import torch.distributed as dist  # noqa: E402
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 / 32x32x2, dense
 HBM_PEAK_GBS = 8000.0
 
+
+def pmc_traffic(workload, kind):
+    """HBM bytes per launch of the roofline kernel, from the rocprofv3 PMC passes of the same bench
+    command (profiles/pmc_traffic.json, written by scripts/pmc_traffic.py: FETCH_SIZE x 2 for the gfx950
+    half-count of wide streaming reads + WRITE_SIZE, MI355X_MICROARCH.md HBM section), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        return json.load(open(path))[f"{workload}/{kind}"]["bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
+
 WORKLOADS = {
     # BASELINE.json configs[1]
     "cfg2": dict(model=dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=4,
@@ -119,6 +130,7 @@ def main():
     ap.add_argument("--points", type=int, default=0, help="override points per sample")
     ap.add_argument("--roofline-kernel", default="moe_bwd", choices=["moe_fwd", "moe_bwd", "wgrad"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--breakdown", action="store_true", help="print per-kernel-class device time to stderr")
     args = ap.parse_args()
 
@@ -141,34 +153,77 @@ def main():
     model = GNOT(*[m[k] for k in ("input_dim", "theta_dim", "input_func_dim", "out_dim", "n_attn_layers",
                                   "n_attn_hidden_dim", "n_mlp_num_layers", "n_mlp_hidden_dim",
                                   "n_input_hidden_dim", "n_expert", "n_head", "n_input_functions")]).to(device)
-    opt = torch.optim.AdamW(model.parameters(), lr=1e-3, fused=True)   # main.py:50-51 (fused kernel)
+    use_graph = not args.no_graph
+    # main.py:50-51 AdamW(lr=1e-3), fused multi-tensor kernel; capturable keeps its step count on device
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-3, fused=True, capturable=use_graph)
     x, x_off, theta, fns, fn_offs, y, seg = make_batch(w, 100 + rank, device)
     B = w["B"]
     eng = model.engine()
-    if world > 1:
-        eng.grad_hook = lambda g: dist.all_reduce(g, op=dist.ReduceOp.AVG)
 
-    def step():
+    # one training step = [forward + RelL2 + backward] -> (N>1: ONE all-reduce of the flat gradient
+    # buffer, sample-DP) -> [AdamW].  With hipGraphs the two bracketed parts are captured once and
+    # replayed; the collective stays an eager RCCL call between them.
+    def fwd_bwd():
         out = model.forward_packed(x, x_off, theta, fns, fn_offs)
         loss = rel_l2_loss(out, y, seg, B)
         opt.zero_grad(set_to_none=True)
         loss.backward()
-        opt.step()
         return loss
 
-    for _ in range(args.warmup):
-        step()
+    def allreduce():
+        if world > 1:
+            dist.all_reduce(eng.grad_flat, op=dist.ReduceOp.AVG)
+
+    def eager_step():
+        fwd_bwd()
+        allreduce()
+        opt.step()
+
+    # warm-up (also the capture warm-up: allocations, plan binding, optimizer state)
+    side = torch.cuda.Stream(device)
+    side.wait_stream(torch.cuda.current_stream(device))
+    with torch.cuda.stream(side):
+        for _ in range(max(args.warmup, 2)):
+            eager_step()
+    torch.cuda.current_stream(device).wait_stream(side)
     torch.cuda.synchronize()
     if args.breakdown:
         for kind in ("moe_fwd", "moe_bwd", "wgrad"):
             eng.profile_enable(kind)
-            step()
+            eager_step()
             ms, n, fl = eng.profile_read()
             print(f"[breakdown] {kind}: {ms:.3f} ms/step over {n} launches, "
                   f"{fl / ms / 1e9 if ms else 0:.1f} TFLOP/s", file=sys.stderr)
         eng.profile_enable("")
         torch.cuda.synchronize()
-    eng.profile_enable(args.roofline_kernel)
+
+    step = eager_step
+    if use_graph:
+        # the roofline kernel's hipEvent pairs are recorded inside the captured graph, so the timed
+        # replays carry them (the pool of events exists from one eager profiled step)
+        eng.profile_enable(args.roofline_kernel)
+        eager_step()
+        eng.profile_read()
+        torch.cuda.synchronize()
+        eng.profile_enable(args.roofline_kernel)
+        g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_fb):
+            fwd_bwd()
+        with torch.cuda.graph(g_opt, pool=g_fb.pool()):
+            opt.step()
+        torch.cuda.synchronize()
+
+        def graph_step():
+            g_fb.replay()
+            allreduce()
+            g_opt.replay()
+        step = graph_step
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize()
+    else:
+        eng.profile_enable(args.roofline_kernel)
+
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -179,6 +234,8 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # eager: summed over every timed step; graph: the events hold the LAST replay's launches, and
+    # launches/flops are those of one step -> both give the average launch duration
     kms, klaunch, kflops = eng.profile_read()
     eng.profile_enable("")
     if world > 1:
@@ -187,7 +244,7 @@ def main():
         elapsed = float(t.item())
     pts = B * w["N"] * args.steps * world
     avg_launch_ms = kms / max(klaunch, 1)
-    achieved = (kflops / max(klaunch, 1)) / (avg_launch_ms * 1e-3) / 1e12 if klaunch else 0.0
+    achieved = (kflops / max(klaunch, 1)) / (avg_launch_ms * 1e-3) / 1e12 if klaunch and kms > 0 else 0.0
     result = {
         "metric": "mesh points/sec (GNOT fwd+bwd, whole node)",
         "value": round(pts / elapsed, 1),
@@ -207,17 +264,17 @@ def main():
                    "heads": m["n_head"], "blocks": m["n_attn_layers"], "mlp_layers": m["n_mlp_num_layers"],
                    "input_functions": m["n_input_functions"],
                    "parallelism": f"sample-dp{world}" if world > 1 else "single",
-                   "step": "pack+fwd+RelL2+bwd+AdamW"},
+                   "step": "pack+fwd+RelL2+bwd+AdamW" + (" (hipGraph replay)" if use_graph else " (eager)")},
         "roofline": {
             "kernel": {"moe_fwd": "chain_fwd_kernel (fused MoE expert chains, forward)",
                        "moe_bwd": "chain_bwd_kernel (fused MoE expert chains, backward)",
-                       "wgrad": "wgrad_kernel+wgrad_reduce_kernel (weight gradients)"}[args.roofline_kernel],
+                       "wgrad": "pgemm_kernel+pgemm_reduce_kernel (weight gradients)"}[args.roofline_kernel],
             "bound": "mfma",
             "achieved": round(achieved, 3),
             "peak": FP32_MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s",
             "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
-            "traffic": None,
+            "traffic": None if args.points else pmc_traffic(args.workload, args.roofline_kernel),
             "avg_launch_us": round(avg_launch_ms * 1e3, 2),
             "flops_per_launch": kflops / max(klaunch, 1),
             "launches": klaunch,

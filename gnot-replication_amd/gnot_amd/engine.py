@@ -38,6 +38,7 @@ class Engine:
         self.grad_views = None
         self.grad_arena = None     # flat fp32 view of every parameter gradient (one buffer)
         self.grad_hook = None      # optional callable(grad_arena) run after the backward kernels
+        self.grad_flat = None      # the flat copy of the arena handed to autograd by the last backward
         self.fwd_token = 0
 
     def __del__(self):

@@ -101,6 +101,7 @@ class _GNOTFunction(torch.autograd.Function):
         # ONE copy of the whole gradient arena (the workspace is reused by the next step); every
         # parameter gradient is a view of that fresh buffer
         flat = eng.grad_arena.clone()
+        eng.grad_flat = flat        # the step's gradient buffer (sample-DP all-reduces it in place)
         ws, bs = [], []
         for off_w, off_b, shape_w, nb in eng.grad_layout:
             ws.append(flat[off_w:off_w + shape_w[0] * shape_w[1]].view(shape_w))
