@@ -158,6 +158,19 @@ struct gnot_plan {
   bool packed = false;
   bool fwd_done = false;
 
+  // point sharding (gnot_plan_set_shard): sample b's points are split over `world` ranks
+  int world = 1, rank = 0;
+  gnot_comm comm{};
+  std::vector<long> nglob;                 // [B] global points per sample (sharded batches)
+  bool sharded = false;                    // world > 1 for the current batch
+  std::vector<CopySeg> xsend, xrecv;       // scramble all-to-all: hm -> send buffer, recv buffer -> tokens
+  std::vector<int> xsend_prefix, xrecv_prefix;   // float4 prefix sums for the copy kernel
+  std::vector<int64_t> xsend_counts, xrecv_counts;
+  CopySeg* d_xsend = nullptr;
+  CopySeg* d_xrecv = nullptr;
+  int* d_xsend_prefix = nullptr;
+  int* d_xrecv_prefix = nullptr;
+
   // live kernel timing (bench roofline): hipEvents around every launch of one kernel class
   std::string prof_kind;
   std::vector<hipEvent_t> prof_events;   // pool, pairs
@@ -722,6 +735,126 @@ static void build_attn_tables(gnot_plan* p) {
   }
 }
 
+// ====================================================================== point sharding
+static void shard_range(long n, int rank, int world, long& lo, long& hi) {
+  lo = n * rank / world;
+  hi = n * (rank + 1) / world;
+}
+
+// The scramble all-to-all of one rank (see gnot_hip.h).  Flat row r = h*N_b + n of sample b's
+// head-major [H, N_b, dh] apply output belongs to output token r / H.  Rank s computes the rows of
+// its points n in [lo_s, hi_s) (local head-major layout: loff_s*d + (h*cnt_s + n - lo_s)*dh); rank t
+// owns the tokens [lo_t, hi_t), i.e. flat rows [lo_t*H, hi_t*H), stored in token order at
+// loff_t*d + (r - lo_t*H)*dh.  For every (peer, sample, head) the intersection is ONE contiguous run
+// on both sides; packets are ordered (peer, sample, head) on both sides.
+static void build_exchange(int B, const std::vector<long>& nglob, int H, int dh, int me, int world,
+                           std::vector<CopySeg>& send, std::vector<CopySeg>& recv, std::vector<int64_t>& send_counts,
+                           std::vector<int64_t>& recv_counts) {
+  const long d = (long)H * dh;
+  std::vector<std::vector<long>> lo(world, std::vector<long>(B)), hi = lo, loff = lo;
+  for (int r = 0; r < world; ++r) {
+    long acc = 0;
+    for (int b = 0; b < B; ++b) {
+      shard_range(nglob[b], r, world, lo[r][b], hi[r][b]);
+      loff[r][b] = acc;
+      acc += hi[r][b] - lo[r][b];
+    }
+  }
+  send.clear(); recv.clear();
+  send_counts.assign(world, 0);
+  recv_counts.assign(world, 0);
+  long scur = 0, rcur = 0;
+  auto run = [&](int s, int t, int b, int h, long& r0, long& r1) {
+    const long N = nglob[b];
+    r0 = std::max((long)h * N + lo[s][b], lo[t][b] * H);
+    r1 = std::min((long)h * N + hi[s][b], hi[t][b] * H);
+    return r0 < r1;
+  };
+  for (int t = 0; t < world; ++t)          // me = source
+    for (int b = 0; b < B; ++b)
+      for (int h = 0; h < H; ++h) {
+        long r0, r1;
+        if (!run(me, t, b, h, r0, r1)) continue;
+        const long cnt = hi[me][b] - lo[me][b];
+        const long len = (r1 - r0) * dh;
+        send.push_back(CopySeg{loff[me][b] * d + (h * cnt + (r0 - (long)h * nglob[b] - lo[me][b])) * dh, scur, len});
+        scur += len;
+        send_counts[t] += len;
+      }
+  for (int s = 0; s < world; ++s)          // me = destination
+    for (int b = 0; b < B; ++b)
+      for (int h = 0; h < H; ++h) {
+        long r0, r1;
+        if (!run(s, me, b, h, r0, r1)) continue;
+        const long len = (r1 - r0) * dh;
+        recv.push_back(CopySeg{rcur, loff[me][b] * d + (r0 - lo[me][b] * H) * dh, len});
+        rcur += len;
+        recv_counts[s] += len;
+      }
+}
+
+static std::vector<int> seg_prefix4(const std::vector<CopySeg>& segs) {
+  std::vector<int> pre;
+  int acc = 0;
+  for (const auto& sg : segs) {
+    pre.push_back(acc);
+    acc += (int)(sg.len / 4);
+  }
+  pre.push_back(acc);
+  return pre;
+}
+
+extern "C" int gnot_shard_range(int64_t n, int rank, int world, int64_t* lo, int64_t* hi) {
+  if (world < 1 || rank < 0 || rank >= world || n < 0 || !lo || !hi) return fail(GNOT_E_INVALID, "bad shard range");
+  long l, h;
+  shard_range(n, rank, world, l, h);
+  *lo = l;
+  *hi = h;
+  return GNOT_OK;
+}
+
+extern "C" int gnot_shard_exchange(int B, const int64_t* n_global, int n_head, int head_dim, int rank, int world,
+                                   int64_t* send_counts, int64_t* recv_counts, int64_t* segs, int64_t cap,
+                                   int64_t* nseg) {
+  if (B <= 0 || !n_global || n_head <= 0 || head_dim <= 0 || world < 1 || rank < 0 || rank >= world || !nseg)
+    return fail(GNOT_E_INVALID, "bad shard exchange arguments");
+  std::vector<long> ng(n_global, n_global + B);
+  std::vector<CopySeg> snd, rcv;
+  std::vector<int64_t> sc, rc;
+  build_exchange(B, ng, n_head, head_dim, rank, world, snd, rcv, sc, rc);
+  if (send_counts) std::copy(sc.begin(), sc.end(), send_counts);
+  if (recv_counts) std::copy(rc.begin(), rc.end(), recv_counts);
+  *nseg = (int64_t)(snd.size() + rcv.size());
+  int64_t k = 0;
+  for (int dir = 0; dir < 2; ++dir)
+    for (const auto& sg : dir == 0 ? snd : rcv) {
+      if (segs && k < cap) {
+        segs[4 * k] = dir;
+        segs[4 * k + 1] = dir == 0 ? sg.a : sg.b;    // local offset (hm for send, tokens for recv)
+        segs[4 * k + 2] = dir == 0 ? sg.b : sg.a;    // buffer offset
+        segs[4 * k + 3] = sg.len;
+      }
+      ++k;
+    }
+  return GNOT_OK;
+}
+
+extern "C" int gnot_plan_set_shard(gnot_plan* p, int rank, int world, int B, const int64_t* n_global,
+                                   const gnot_comm* comm) {
+  if (!p) return fail(GNOT_E_INVALID, "null plan");
+  if (world <= 1 || !comm) {
+    p->world = 1; p->rank = 0; p->nglob.clear(); p->comm = gnot_comm{};
+    return GNOT_OK;
+  }
+  if (rank < 0 || rank >= world || B <= 0 || !n_global || !comm->allreduce_sum || !comm->alltoallv)
+    return fail(GNOT_E_INVALID, "bad shard arguments");
+  p->world = world;
+  p->rank = rank;
+  p->comm = *comm;
+  p->nglob.assign(n_global, n_global + B);
+  return GNOT_OK;
+}
+
 extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, const int64_t* fn_off,
                                    int training) {
   if (!p || B <= 0 || !x_off) return fail(GNOT_E_INVALID, "bad batch arguments");
@@ -744,6 +877,22 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
   if (p->P <= 0) return fail(GNOT_E_INVALID, "empty batch (no query points)");
   if (p->P >= (1L << 31) / 4) return fail(GNOT_E_INVALID, "batch too large for 32-bit segment indices");
   p->training = training != 0;
+  p->sharded = p->world > 1;
+  if (p->sharded) {
+    if ((int)p->nglob.size() != B) return fail(GNOT_E_INVALID, "gnot_plan_set_shard was declared for another B");
+    for (int b = 0; b < B; ++b) {
+      long lo, hi;
+      shard_range(p->nglob[b], p->rank, p->world, lo, hi);
+      if (p->xoff[b + 1] - p->xoff[b] != hi - lo)
+        return fail(GNOT_E_INVALID, "x_off does not match this rank's shard of n_global (gnot_shard_range)");
+    }
+    build_exchange(B, p->nglob, p->H, p->dh, p->rank, p->world, p->xsend, p->xrecv, p->xsend_counts,
+                   p->xrecv_counts);
+    p->xsend_prefix = seg_prefix4(p->xsend);
+    p->xrecv_prefix = seg_prefix4(p->xrecv);
+  } else {
+    p->xsend.clear(); p->xrecv.clear(); p->xsend_prefix.clear(); p->xrecv_prefix.clear();
+  }
 
   // ---------------- workspace carve
   plan_images(p);
@@ -807,6 +956,10 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
     C.add(s + "query2", P * D, D);
   }
   C.add("stage", E * P * D, D);
+  if (p->sharded) {                          // scramble exchange scratch: head-major rows / packed peers
+    C.add("xa", P * D, D);
+    C.add("xb", P * D, D);
+  }
   // attention segments
   make_chunks(p->xoff, p->qchunks, p->qchunk_off);
   p->fchunks.assign(I, {});
@@ -876,6 +1029,8 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
   tbl(p->qchunk_off.size() * sizeof(int));
   for (int i = 0; i < I; ++i) { tbl(p->fchunks[i].size() * sizeof(int4)); tbl(p->fchunk_off[i].size() * sizeof(int)); }
   tbl((p->B + 1) * sizeof(long) * (1 + I));
+  tbl(p->xsend.size() * sizeof(CopySeg)); tbl(p->xrecv.size() * sizeof(CopySeg));
+  tbl(p->xsend_prefix.size() * sizeof(int)); tbl(p->xrecv_prefix.size() * sizeof(int));
 
   // point-reduction GEMM groups: built with null buffer pointers now (sizes only), rebuilt with
   // real pointers at bind
@@ -1007,6 +1162,10 @@ extern "C" int gnot_plan_bind_workspace(gnot_plan* p, void* workspace, size_t by
   p->d_kvbwd_jobs = static_cast<AttnKVBwdArgs*>(put(p->kvbwd_jobs.data(), p->kvbwd_jobs.size() * sizeof(AttnKVBwdArgs)));
   p->d_dfn_jobs.clear();
   for (auto& v : p->dfn_jobs) p->d_dfn_jobs.push_back(static_cast<LinearArgs*>(put(v.data(), v.size() * sizeof(LinearArgs))));
+  p->d_xsend = static_cast<CopySeg*>(put(p->xsend.data(), p->xsend.size() * sizeof(CopySeg)));
+  p->d_xrecv = static_cast<CopySeg*>(put(p->xrecv.data(), p->xrecv.size() * sizeof(CopySeg)));
+  p->d_xsend_prefix = static_cast<int*>(put(p->xsend_prefix.data(), p->xsend_prefix.size() * sizeof(int)));
+  p->d_xrecv_prefix = static_cast<int*>(put(p->xrecv_prefix.data(), p->xrecv_prefix.size() * sizeof(int)));
   if (cur > p->table_bytes) return fail(GNOT_E_INVALID, "internal: table overflow");
   GNOT_CK(hipMemcpy(tp, host.data(), cur, hipMemcpyHostToDevice));
   if (p->training && !p->side) GNOT_CK(hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
@@ -1152,6 +1311,36 @@ int run_wgrad_side(Ctx& c, const WgradGroup& G, std::initializer_list<const floa
   return GNOT_OK;
 }
 
+// sum a state buffer over the ranks of a sharded batch
+int shard_allreduce(Ctx& c, float* buf, long count) {
+  gnot_plan* p = c.p;
+  if (!p->sharded || count <= 0) return GNOT_OK;
+  if (p->comm.allreduce_sum(p->comm.user, buf, count, c.s) != 0)
+    return fail(GNOT_E_HIP, "gnot_comm.allreduce_sum failed");
+  return GNOT_OK;
+}
+
+// forward scramble: local head-major apply output `hm` -> this rank's output tokens `tok`
+// backward (reverse): token-order gradient `tok` -> local head-major `hm`
+int shard_exchange(Ctx& c, float* hm, float* tok, bool reverse) {
+  gnot_plan* p = c.p;
+  float* xa = p->P_("xa");
+  float* xb = p->P_("xb");
+  const int ns = (int)p->xsend.size(), nr = (int)p->xrecv.size();
+  if (!reverse) {
+    GNOT_CK(launch_segcopy(p->d_xsend, p->d_xsend_prefix, ns, p->xsend_prefix.back(), hm, xa, false, c.s));
+    if (p->comm.alltoallv(p->comm.user, xa, p->xsend_counts.data(), xb, p->xrecv_counts.data(), c.s) != 0)
+      return fail(GNOT_E_HIP, "gnot_comm.alltoallv failed");
+    GNOT_CK(launch_segcopy(p->d_xrecv, p->d_xrecv_prefix, nr, p->xrecv_prefix.back(), xb, tok, false, c.s));
+  } else {
+    GNOT_CK(launch_segcopy(p->d_xrecv, p->d_xrecv_prefix, nr, p->xrecv_prefix.back(), tok, xb, true, c.s));
+    if (p->comm.alltoallv(p->comm.user, xb, p->xrecv_counts.data(), xa, p->xsend_counts.data(), c.s) != 0)
+      return fail(GNOT_E_HIP, "gnot_comm.alltoallv failed");
+    GNOT_CK(launch_segcopy(p->d_xsend, p->d_xsend_prefix, ns, p->xsend_prefix.back(), xa, hm, true, c.s));
+  }
+  return GNOT_OK;
+}
+
 #define GNOT_RUN(expr)              \
   do {                              \
     const int rc_ = (expr);         \
@@ -1174,18 +1363,20 @@ int attn_forward(Ctx& c, int l, bool cross, const float* q_in, float* res_out, f
     // keys/values/states of the input functions were computed for every block up front
     for (int i = 0; i < p->I; ++i) ap.state[i] = p->P_(s + "cstate" + std::to_string(i));
     ap.q = q; ap.ldq = D; ap.nsrc = p->I; ap.chunks = p->d_qchunks; ap.nchunks = nq; ap.off = p->d_xoff;
-    ap.H = p->H; ap.dh = p->dh; ap.res = res_out;
+    ap.H = p->H; ap.dh = p->dh; ap.res = p->sharded ? p->P_("xb") : res_out;
     GNOT_CK(launch_attn_apply_fwd(ap, c.s));
   } else {
     float* qkv = p->P_(cross ? s + "cq" : s + "sq");
     GNOT_RUN(run_linear(c, q_in, D, D, A.qkv, pbias + A.bqkv, qkv, 3 * D, 3 * D, P, EPI_STORE, 2 * D));
     float* st = p->P_(cross ? s + "cstate0" : s + "sstate");
     GNOT_RUN(run_state(c, cross ? p->st_c[l][0] : p->st_s[l]));
+    GNOT_RUN(shard_allreduce(c, st, (long)p->B * p->H * (p->dh * p->dh + p->dh)));   // S, z over all ranks
     AttnApplyArgs ap{};
     ap.q = qkv; ap.ldq = 3 * D; ap.nsrc = 1; ap.state[0] = st; ap.chunks = p->d_qchunks; ap.nchunks = nq;
-    ap.off = p->d_xoff; ap.H = p->H; ap.dh = p->dh; ap.res = res_out;
+    ap.off = p->d_xoff; ap.H = p->H; ap.dh = p->dh; ap.res = p->sharded ? p->P_("xb") : res_out;
     GNOT_CK(launch_attn_apply_fwd(ap, c.s));
   }
+  if (p->sharded) GNOT_RUN(shard_exchange(c, p->P_("xb"), res_out, false));   // the scramble, across ranks
   GNOT_RUN(run_linear(c, res_out, D, D, A.o, pbias + A.bo, out, D, D, P, EPI_STORE, 0));
   return GNOT_OK;
 }
@@ -1205,8 +1396,12 @@ int attn_backward(Ctx& c, int l, bool cross) {
   float* dqkv = p->P_(p->dqkv_buf(cross));
   const int nq = (int)p->qchunks.size();
   GNOT_RUN(guard_write(c, dqkv));
-  // fc_out backward-data: dres = dout W_o
+  // fc_out backward-data: dres = dout W_o (token order); sharded: back to this rank's head-major rows
   GNOT_RUN(run_linear(c, dsum, D, D, p->T_img[lo], nullptr, dres, D, D, P, EPI_STORE, 0));
+  if (p->sharded) {
+    GNOT_RUN(shard_exchange(c, p->P_("xb"), dres, true));
+    dres = p->P_("xb");
+  }
   if (cross && p->I > 0) {
     const float* q = p->P_(s + "cq");
     AttnApplyArgs ap{};
@@ -1235,6 +1430,7 @@ int attn_backward(Ctx& c, int l, bool cross) {
     GNOT_CK(launch_attn_apply_bwd(ap, c.s));
     float* dst = p->P_("dstate0");
     GNOT_RUN(run_state(c, cross ? p->dst_c[l][0] : p->dst_s[l]));
+    GNOT_RUN(shard_allreduce(c, dst, (long)p->B * p->H * (p->dh * p->dh + p->dh)));   // dS, dz over all ranks
     AttnKVBwdArgs kb{};
     kb.k = qkv + D; kb.v = qkv + 2 * D; kb.ldkv = 3 * D; kb.dstate = dst; kb.chunks = p->d_qchunks;
     kb.nchunks = nq; kb.H = p->H; kb.dh = p->dh; kb.dk = dqkv + D; kb.dv = dqkv + 2 * D; kb.lddkv = 3 * D;

@@ -146,5 +146,12 @@ hipError_t launch_concat_theta(const float* x, long ldx, int in_dim, const float
 // out = (base ? base : 0) + sum_e stage[e]
 hipError_t launch_moe_combine(const float* base, const float* stage, long stage_stride, int E,
                               float* out, long n, hipStream_t s);
+// segmented copy: dst[seg.dst + i] = src[seg.src + i], i < seg.len (floats, multiples of 4);
+// reverse swaps the roles of src/dst offsets.  prefix4: float4 prefix sums of the lengths [nseg + 1].
+struct CopySeg {
+  long a, b, len;      // a = source offset, b = destination offset (forward direction)
+};
+hipError_t launch_segcopy(const CopySeg* segs, const int* prefix4, int nseg, int total4, const float* src, float* dst,
+                          bool reverse, hipStream_t s);
 
 }  // namespace gnot

@@ -3,6 +3,8 @@
 //                  broadcast per sample over that sample's points — packed offsets, no padding)
 //   moe_combine  : q_out = q_in + sum_e stage[e]           (reference model.py:129-131, 135-137)
 //                  (q_in may be null: plain sum, used for the expert-summed dX of the MoE backward)
+//   segcopy      : table-driven float4 copy of contiguous runs (the point-shard scramble all-to-all's
+//                  pack / unpack, engine.cpp build_exchange)
 #include "gnot_common.h"
 #include "gnot_kernels.h"
 
@@ -62,6 +64,31 @@ hipError_t launch_moe_combine(const float* base, const float* stage, long stage_
   hipLaunchKernelGGL(moe_combine_kernel, dim3((unsigned)blocks), dim3(256), 0, s,
                      reinterpret_cast<const float4*>(base), reinterpret_cast<const float4*>(stage),
                      stage_stride / 4, E, reinterpret_cast<float4*>(out), n4);
+  return hipGetLastError();
+}
+
+__global__ void __launch_bounds__(256) segcopy_kernel(const CopySeg* __restrict__ segs, const int* __restrict__ prefix4,
+                                                      int nseg, int total4, const float* __restrict__ src,
+                                                      float* __restrict__ dst, int reverse) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total4; i += gridDim.x * 256) {
+    int lo = 0, hi = nseg - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (prefix4[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    const CopySeg sg = segs[lo];
+    const long off = (long)(i - prefix4[lo]) * 4;
+    const long so = reverse ? sg.b : sg.a, dof = reverse ? sg.a : sg.b;
+    *reinterpret_cast<float4*>(dst + dof + off) = *reinterpret_cast<const float4*>(src + so + off);
+  }
+}
+
+hipError_t launch_segcopy(const CopySeg* segs, const int* prefix4, int nseg, int total4, const float* src, float* dst,
+                          bool reverse, hipStream_t s) {
+  if (nseg <= 0 || total4 <= 0) return hipSuccess;
+  const int blocks = std::min((total4 + 255) / 256, 4096);
+  hipLaunchKernelGGL(segcopy_kernel, dim3(blocks), dim3(256), 0, s, segs, prefix4, nseg, total4, src, dst,
+                     reverse ? 1 : 0);
   return hipGetLastError();
 }
 

@@ -27,8 +27,17 @@ EXPORTS = [
     "gnot_plan_bind_params", "gnot_plan_set_batch", "gnot_plan_workspace_bytes",
     "gnot_plan_bind_workspace", "gnot_plan_grad_offsets", "gnot_pack_weights", "gnot_forward",
     "gnot_backward", "gnot_profile_enable", "gnot_profile_read", "gnot_debug_buffer", "gnot_last_error",
-    "gnot_version",
+    "gnot_version", "gnot_plan_set_shard", "gnot_shard_range", "gnot_shard_exchange",
 ]
+
+# gnot_comm callbacks (include/gnot_hip.h)
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p)
+ALLTOALLV_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64),
+                                ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.c_void_p)
+
+
+class GnotComm(ctypes.Structure):
+    _fields_ = [("user", ctypes.c_void_p), ("allreduce_sum", ALLREDUCE_FN), ("alltoallv", ALLTOALLV_FN)]
 
 
 def build(jobs=8, quiet=True):
@@ -61,6 +70,10 @@ def _declare(lib):
     lib.gnot_profile_read.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i64),
                                       ctypes.POINTER(ctypes.c_double)]
     lib.gnot_debug_buffer.argtypes = [P, ctypes.c_char_p, ctypes.POINTER(P), ctypes.POINTER(i64)]
+    lib.gnot_plan_set_shard.argtypes = [P, i32, i32, i32, ctypes.POINTER(i64), ctypes.POINTER(GnotComm)]
+    lib.gnot_shard_range.argtypes = [i64, i32, i32, ctypes.POINTER(i64), ctypes.POINTER(i64)]
+    lib.gnot_shard_exchange.argtypes = [i32, ctypes.POINTER(i64), i32, i32, i32, i32, ctypes.POINTER(i64),
+                                        ctypes.POINTER(i64), ctypes.POINTER(i64), i64, ctypes.POINTER(i64)]
     lib.gnot_last_error.restype = ctypes.c_char_p
     lib.gnot_last_error.argtypes = []
     lib.gnot_version.restype = ctypes.c_char_p

@@ -39,6 +39,7 @@ class Engine:
         self.grad_arena = None     # flat fp32 view of every parameter gradient (one buffer)
         self.grad_hook = None      # optional callable(grad_arena) run after the backward kernels
         self.grad_flat = None      # the flat copy of the arena handed to autograd by the last backward
+        self.comm = None           # parallel.PointShardComm when points are sharded over ranks
         self.fwd_token = 0
 
     def __del__(self):
@@ -62,13 +63,23 @@ class Engine:
             self._bound_ptrs = ptrs
             self.geom = None   # workspace tables embed parameter pointers: rebind
 
-    def prepare(self, x_off, fn_offs, training, device):
-        """Set batch geometry (host int lists) and (re)bind the workspace when it changed."""
+    def prepare(self, x_off, fn_offs, training, device, n_global=None):
+        """Set batch geometry (host int lists) and (re)bind the workspace when it changed.
+        n_global: per-sample global point counts when the points are sharded over ranks (self.comm)."""
         self._bind_params()
-        geom = (tuple(x_off), tuple(tuple(o) for o in fn_offs), bool(training))
+        geom = (tuple(x_off), tuple(tuple(o) for o in fn_offs), bool(training),
+                tuple(n_global) if n_global is not None else None)
         if geom == self.geom:
             return
         B = len(x_off) - 1
+        if self.comm is not None:
+            if n_global is None or len(n_global) != B:
+                raise ValueError("point-sharded GNOT needs n_global (global points of every sample)")
+            ng = (ctypes.c_int64 * B)(*[int(n) for n in n_global])
+            _lib.check(self.lib.gnot_plan_set_shard(self.plan, self.comm.rank, self.comm.world, B, ng,
+                                                    ctypes.byref(self.comm.struct)))
+        else:
+            _lib.check(self.lib.gnot_plan_set_shard(self.plan, 0, 1, 0, None, None))
         xo = (ctypes.c_int64 * (B + 1))(*x_off)
         flat = [v for o in fn_offs for v in o]
         fo = (ctypes.c_int64 * max(1, len(flat)))(*flat) if flat else None
@@ -79,6 +90,8 @@ class Engine:
             self.ws = torch.empty(need + 256, dtype=torch.uint8, device=device)
         torch.cuda.current_stream(device).synchronize()
         _lib.check(self.lib.gnot_plan_bind_workspace(self.plan, self.ws.data_ptr(), self.ws.numel()))
+        if self.comm is not None:
+            self.comm.ws = self.ws
         self.geom = geom
         self.grad_views = None
         self.grad_arena = None

@@ -168,10 +168,18 @@ class GNOT(nn.Module):
         out = self.forward_packed(x.reshape(B * N, x.shape[-1]), x_off, theta, fns, fn_offs)
         return out.view(B, N, -1)
 
-    def forward_packed(self, x, x_off, theta, fns=(), fn_offs=()):
+    def set_point_shard(self, comm):
+        """Shard every sample's points over the ranks of `comm` (gnot_amd.parallel.PointShardComm), or
+        None to switch sharding off.  forward_packed then takes this rank's slices plus n_global."""
+        self.engine().comm = comm
+        self.engine().geom = None
+
+    def forward_packed(self, x, x_off, theta, fns=(), fn_offs=(), n_global=None):
         """Packed-offsets forward (no padding): x [sum N_b, input_dim] with host offsets x_off [B+1];
         fns[i] [sum M_ib, input_func_dim] with fn_offs[i] [B+1].  Equals one B=1 reference call per
-        sample, concatenated.  Returns [sum N_b, out_dim]."""
+        sample, concatenated.  Returns [sum N_b, out_dim].
+        Point-sharded (set_point_shard): x holds this rank's slice of every sample (parallel.shard_range)
+        and n_global the samples' global point counts; the input functions are passed whole."""
         if not x.is_cuda:
             raise RuntimeError("gnot_amd runs on a ROCm GPU only (libgnot_hip.so); no CPU path")
         x = x.contiguous().float()
@@ -180,5 +188,6 @@ class GNOT(nn.Module):
         params = [l.weight for l in self.linears()] + [l.bias for l in self.linears()]
         training = torch.is_grad_enabled() and any(p.requires_grad for p in params)
         eng = self.engine()
-        eng.prepare([int(v) for v in x_off], [[int(v) for v in o] for o in fn_offs], training, x.device)
+        eng.prepare([int(v) for v in x_off], [[int(v) for v in o] for o in fn_offs], training, x.device,
+                    n_global=None if n_global is None else [int(n) for n in n_global])
         return _GNOTFunction.apply(eng, x, theta, fns, self._cfg["out_dim"], *params)

@@ -1,0 +1,157 @@
+"""Multi-GPU host logic of the GNOT hot path.  One process per GPU.
+
+Two modes, both with ONE gradient all-reduce of the flat gradient buffer per step:
+
+* sample data parallel (small meshes, BASELINE configs[1]/[4]): every rank owns whole meshes
+  (`lpt_partition` balances them by point count); gradients are averaged / summed.
+* point sharding (one large mesh, configs[3]): every sample's points are split over the ranks
+  (`shard_range`); the engine calls back into `PointShardComm` for the two exchanges the reference's
+  attention needs (include/gnot_hip.h: state all-reduce, scramble all-to-all) and the caller sums
+  gradients over ranks.  `rel_l2_loss_sharded` is the reference loss (loss.py:14-23) on a sharded
+  mesh: its per-sample sums are all-reduced.
+
+The reference itself is single-device (main.py:27); nothing here has a reference counterpart beyond
+the arithmetic it must reproduce.
+"""
+import ctypes
+import heapq
+import traceback
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import _lib
+
+
+def shard_range(n, rank, world):
+    """[lo, hi) of the points of an n-point sample owned by `rank` (gnot_shard_range)."""
+    lo, hi = ctypes.c_int64(), ctypes.c_int64()
+    _lib.check(_lib.load().gnot_shard_range(int(n), int(rank), int(world), ctypes.byref(lo), ctypes.byref(hi)))
+    return lo.value, hi.value
+
+
+def shard_offsets(n_global, rank, world):
+    """Local packed offsets [B+1] of this rank's slices, and the (lo, hi) range of every sample."""
+    ranges = [shard_range(n, rank, world) for n in n_global]
+    off = [0]
+    for lo, hi in ranges:
+        off.append(off[-1] + hi - lo)
+    return off, ranges
+
+
+def exchange_plan(n_global, n_head, head_dim, rank, world):
+    """This rank's side of the scramble all-to-all (gnot_shard_exchange): send/recv counts per peer
+    (floats) and the copy segments [k, 4] = (dir, local_off, buf_off, len)."""
+    lib = _lib.load()
+    B = len(n_global)
+    ng = (ctypes.c_int64 * B)(*[int(n) for n in n_global])
+    sc, rc = (ctypes.c_int64 * world)(), (ctypes.c_int64 * world)()
+    nseg = ctypes.c_int64()
+    _lib.check(lib.gnot_shard_exchange(B, ng, n_head, head_dim, rank, world, sc, rc, None, 0, ctypes.byref(nseg)))
+    segs = (ctypes.c_int64 * (4 * max(nseg.value, 1)))()
+    _lib.check(lib.gnot_shard_exchange(B, ng, n_head, head_dim, rank, world, sc, rc, segs, nseg.value,
+                                       ctypes.byref(nseg)))
+    arr = np.frombuffer(segs, dtype=np.int64)[: 4 * nseg.value].reshape(-1, 4).copy()
+    return list(sc), list(rc), arr
+
+
+def lpt_partition(sizes, world):
+    """Longest-processing-time assignment of samples (point counts) to ranks: biggest first onto the
+    least-loaded rank (ties -> lowest rank).  Returns per-rank lists of sample indices (ascending)."""
+    heap = [(0, r) for r in range(world)]
+    out = [[] for _ in range(world)]
+    for i in sorted(range(len(sizes)), key=lambda i: (-sizes[i], i)):
+        load, r = heapq.heappop(heap)
+        out[r].append(i)
+        heapq.heappush(heap, (load + sizes[i], r))
+    return [sorted(v) for v in out]
+
+
+class PointShardComm:
+    """gnot_comm backed by a torch.distributed process group.
+
+    The engine hands over raw pointers into its workspace; they are wrapped as float32 views of the
+    workspace tensor (no copies).  With RCCL (`nccl` backend) the collectives are ordered on the
+    current HIP stream by torch.  `stage_via_host` routes them through host tensors instead (for the
+    gloo backend, e.g. several ranks sharing one GPU in tests)."""
+
+    def __init__(self, group=None, stage_via_host=False):
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.stage = stage_via_host
+        self.ws = None                        # the engine's uint8 workspace tensor (set by Engine)
+        self._ar = _lib.ALLREDUCE_FN(self._allreduce)
+        self._a2a = _lib.ALLTOALLV_FN(self._alltoallv)
+        self.struct = _lib.GnotComm(None, self._ar, self._a2a)
+
+    def _view(self, ptr, n):
+        off = int(ptr) - self.ws.data_ptr()
+        if off < 0 or off % 4 or off + 4 * n > self.ws.numel():
+            raise RuntimeError("gnot_comm buffer outside the engine workspace")
+        return self.ws[off: off + 4 * n].view(torch.float32)
+
+    def _allreduce(self, user, buf, count, stream):
+        try:
+            if count > 0:
+                t = self._view(buf, count)
+                if self.stage:
+                    h = t.cpu()
+                    dist.all_reduce(h, group=self.group)
+                    t.copy_(h)
+                else:
+                    dist.all_reduce(t, group=self.group)
+            return 0
+        except Exception:
+            traceback.print_exc()
+            return -1
+
+    def _alltoallv(self, user, send, send_counts, recv, recv_counts, stream):
+        try:
+            sc = [int(send_counts[i]) for i in range(self.world)]
+            rc = [int(recv_counts[i]) for i in range(self.world)]
+            dev = self.ws.device
+            s = self._view(send, sum(sc)) if sum(sc) else torch.empty(0, device=dev)
+            r = self._view(recv, sum(rc)) if sum(rc) else torch.empty(0, device=dev)
+            if self.stage:
+                hr = torch.empty(sum(rc), dtype=torch.float32)
+                dist.all_to_all_single(hr, s.cpu(), rc, sc, group=self.group)
+                r.copy_(hr)
+            else:
+                dist.all_to_all_single(r, s, rc, sc, group=self.group)
+            return 0
+        except Exception:
+            traceback.print_exc()
+            return -1
+
+
+class _SumOverRanks(torch.autograd.Function):
+    """all-reduce(sum) whose backward is the identity: every rank evaluates the SAME loss from the
+    reduced sums, so d loss / d (local partial) is the gradient of the reduced value itself."""
+
+    @staticmethod
+    def forward(ctx, t, group, stage):
+        out = t.clone()
+        if stage:
+            h = out.cpu()
+            dist.all_reduce(h, group=group)
+            out.copy_(h)
+        else:
+            dist.all_reduce(out, group=group)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None, None
+
+
+def rel_l2_loss_sharded(out, tgt, seg, B, group=None, stage_via_host=False):
+    """RelL2Loss (loss.py:14-23) of meshes whose points are sharded over ranks: per-sample sums of
+    (p - t)^2 and t^2 over ALL ranks' points, then mean over samples x channels of sqrt(num/den)."""
+    C = out.shape[1]
+    num = torch.zeros(B, C, device=out.device, dtype=out.dtype).index_add(0, seg, (out - tgt) ** 2)
+    den = torch.zeros(B, C, device=out.device, dtype=out.dtype).index_add(0, seg, tgt ** 2)
+    num = _SumOverRanks.apply(num, group, stage_via_host)
+    den = _SumOverRanks.apply(den, group, stage_via_host)
+    return (num / den).sqrt().mean()

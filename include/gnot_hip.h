@@ -98,6 +98,44 @@ int gnot_forward(gnot_plan* plan, const float* x, const float* theta, const floa
  * (overwritten) into the gradient arena. */
 int gnot_backward(gnot_plan* plan, const float* dout, void* stream);
 
+/* ---------------------------------------------------------------- point sharding (multi-GPU)
+ * One process per GPU.  Every sample b of a batch is split over `world` ranks in contiguous point
+ * ranges: rank r owns global points [floor(r*N_b/world), floor((r+1)*N_b/world)) (gnot_shard_range).
+ * Everything per point stays local (gating, encoders, projections, MoE chains, residuals); the
+ * reference's attention needs two exchanges:
+ *   - the self-attention states S = sum k^T v, z = sum k (model.py:98-100), and in the backward
+ *     dS, dz, are sums over ALL points of a sample: partial states are all-reduced (sum);
+ *   - the head-major "scramble" of model.py:81/103-104 maps output token n' to flat rows
+ *     n'*H .. n'*H+H-1 of [H, N, dh], i.e. to ALL points of a head range: the apply pass output is
+ *     exchanged all-to-all (and the gradient back in the backward).
+ * The input-function branch of cross attention is replicated on every rank; its backward needs no
+ * exchange (every gradient downstream of dS is linear in it, so the per-rank partials add up in the
+ * caller's gradient all-reduce).  The caller sums the parameter gradients over ranks.
+ * The collectives are caller-provided callbacks (RCCL through torch.distributed in gnot_amd); they
+ * are invoked synchronously from gnot_forward / gnot_backward and must be ordered on `stream`. */
+typedef struct gnot_comm {
+  void* user;
+  /* in-place sum over ranks of `count` floats */
+  int (*allreduce_sum)(void* user, float* buf, int64_t count, void* stream);
+  /* all-to-all-v: send_counts[t] floats to rank t (packed in rank order in `send`), receive
+   * recv_counts[s] floats from rank s (packed in rank order into `recv`) */
+  int (*alltoallv)(void* user, const float* send, const int64_t* send_counts, float* recv,
+                   const int64_t* recv_counts, void* stream);
+} gnot_comm;
+
+/* Declare the rank's shard of the next batch: n_global[b] = points of sample b over all ranks.
+ * Call before gnot_plan_set_batch, whose x_off then gives the LOCAL slices (validated against
+ * gnot_shard_range).  world == 1 (or comm == NULL) switches sharding off.  `comm` is copied. */
+int gnot_plan_set_shard(gnot_plan* plan, int rank, int world, int B, const int64_t* n_global, const gnot_comm* comm);
+
+/* Host-only helpers (no GPU): the canonical point range of a rank, and the rank's side of the
+ * scramble all-to-all.  Segments are rows of 4 int64 {dir, local_off, buf_off, len} in floats:
+ * dir 0 copies local head-major apply output -> send buffer, dir 1 copies receive buffer -> local
+ * token-order rows.  *nseg returns the number of segments (at most `cap` are written). */
+int gnot_shard_range(int64_t n, int rank, int world, int64_t* lo, int64_t* hi);
+int gnot_shard_exchange(int B, const int64_t* n_global, int n_head, int head_dim, int rank, int world,
+                        int64_t* send_counts, int64_t* recv_counts, int64_t* segs, int64_t cap, int64_t* nseg);
+
 /* Live kernel timing for the bench's roofline: while enabled, every launch of kernel class `kind`
  * ("moe_fwd" fused expert chains forward, "moe_bwd" their backward, "wgrad" weight-gradient GEMMs;
  * "" disables) is bracketed by hipEvents on its stream.  gnot_profile_read synchronizes on those

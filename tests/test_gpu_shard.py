@@ -1,0 +1,114 @@
+"""Point-sharded GNOT forward + backward through the HIP engine (gnot_plan_set_shard + the
+PointShardComm callbacks): `world` processes share cuda:0 over gloo (host-staged collectives, the
+box has one GPU), each owns a contiguous slice of every sample's points.  The
+gathered outputs and the rank-summed parameter gradients must match the unsharded CPU oracle."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _case(cfg, Ns, Ms, seed):
+    from golden_util import model_args
+    from gnot_amd import GNOT
+    from oracle import gnot_oracle as O
+    torch.manual_seed(seed)
+    ref = GNOT(*model_args(cfg))
+    params = {k: v.double().numpy() for k, v in ref.state_dict().items()}
+    rng = np.random.default_rng(seed)
+    x = rng.random((sum(Ns), cfg["input_dim"]))
+    theta = rng.random((len(Ns), cfg["theta_dim"]))
+    fns = [rng.random((sum(Ms[i]), cfg["input_func_dim"])) for i in range(cfg["n_input_functions"])]
+    off = lambda L: np.concatenate([[0], np.cumsum(L)]).astype(np.int64)
+    G = rng.standard_normal((sum(Ns), cfg["out_dim"]))
+    fx = dict(params=params, cfg=cfg, x=x, x_off=off(Ns), theta=theta, fns=fns,
+              fn_offs=[off(Ms[i]) for i in range(cfg["n_input_functions"])], G=G)
+    out64, g64 = O.gnot_forward_backward(params, cfg, x, fx["x_off"], theta, fns, fx["fn_offs"], G=G)
+    out32, g32 = O.gnot_forward_backward(params, cfg, x, fx["x_off"], theta, fns, fx["fn_offs"], G=G,
+                                         dtype=np.float32)
+    fx["out"], fx["grads"] = out64, g64
+    fx["e32"] = {k: float(np.linalg.norm(g32[k].astype(np.float64) - g64[k])) for k in g64}
+    return fx
+
+
+def _rank(rank, world, port, cfg, Ns, Ms, q):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "gnot-replication_amd"), os.path.join(ROOT, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from golden_util import check_parity, model_args
+        from gnot_amd import GNOT
+        from gnot_amd import parallel as par
+        fx = _case(cfg, Ns, Ms, seed=11)
+        dev = torch.device("cuda", 0)
+        m = GNOT(*model_args(cfg)).to(dev)
+        m.load_state_dict({k: torch.from_numpy(v).float() for k, v in fx["params"].items()})
+        m.set_point_shard(par.PointShardComm(stage_via_host=True))
+        loc_off, ranges = par.shard_offsets(Ns, rank, world)
+        rows = np.concatenate([np.arange(fx["x_off"][b] + lo, fx["x_off"][b] + hi) for b, (lo, hi) in enumerate(ranges)])
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).float().to(dev)
+        out = m.forward_packed(t(fx["x"][rows]), loc_off, t(fx["theta"]), [t(f) for f in fx["fns"]],
+                               [o.tolist() for o in fx["fn_offs"]], n_global=Ns)
+        (out * t(fx["G"][rows])).sum().backward()
+        flat = m.engine().grad_flat
+        h = flat.cpu()
+        dist.all_reduce(h)                     # parameter gradients: sum over ranks
+        flat.copy_(h.to(dev))
+        torch.cuda.synchronize()
+        outs = [None] * world
+        dist.all_gather_object(outs, (rows, out.detach().double().cpu().numpy()))
+        if rank == 0:
+            full = np.zeros_like(fx["out"])
+            for r_rows, o in outs:
+                full[r_rows] = o
+            grads = {k: p.grad.double().cpu().numpy() for k, p in m.named_parameters()}
+            q.put(check_parity(full, grads, fx))
+    except Exception as e:  # report instead of hanging the other rank's collectives
+        if rank == 0:
+            q.put([f"rank0 exception: {e!r}"])
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,case", [
+    (2, dict(cfg=dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=2, n_attn_layers=2, d=64,
+                      n_mlp_num_layers=2, n_expert=3, n_head=8, n_input_functions=1),
+             Ns=[150, 97], Ms=[[40, 31]])),
+    (2, dict(cfg=dict(input_dim=3, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=1, d=64,
+                      n_mlp_num_layers=2, n_expert=2, n_head=4, n_input_functions=0),
+             Ns=[131], Ms=[])),
+    (3, dict(cfg=dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=1, d=32,
+                      n_mlp_num_layers=2, n_expert=2, n_head=8, n_input_functions=2),
+             Ns=[64, 5], Ms=[[20, 9], [7, 12]])),
+])
+def test_point_sharded_gnot_matches_oracle(world, case):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, case["cfg"], case["Ns"], case["Ms"], q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    errs = q.get(timeout=100)
+    for p in procs:
+        p.join(timeout=30)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert not errs, errs
