@@ -5,13 +5,16 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-Workload = BASELINE.json configs[1] (the metric's single-GPU configuration): GNOT with 4 blocks,
-4 experts, hidden 128, 8 heads, 4-layer MLPs, 2 input functions (multi-input cross-attention),
-one 2-D irregular mesh of 10,000 query points per GPU with 805 points per input function, fp32
-(the reference computes in fp32).  A step = pack weights -> GNOT forward (gnot_amd, HIP) -> RelL2
-loss (loss.py:14-23, per-sample segment sums) -> backward to every parameter gradient ->
-(N>1: one RCCL all-reduce of the flat gradient arena, sample-data-parallel) -> AdamW step.
-Multi-GPU scaling is weak: every rank owns its own mesh (SURVEY.md §8e sample-DP).
+Workload (default) = BASELINE.json configs[1] (the metric's single-GPU configuration): GNOT with 4
+blocks, 4 experts, hidden 128, 8 heads, 4-layer MLPs, 2 input functions (multi-input cross-attention),
+one 2-D irregular mesh of 10,000 query points per GPU with 805 points per input function, fp32 (the
+reference computes in fp32).  A step = pack weights -> GNOT forward (gnot_amd, HIP) -> RelL2 loss
+(loss.py:14-23, per-sample segment sums) -> backward to every parameter gradient -> (N>1: one RCCL
+all-reduce of the flat gradient buffer) -> AdamW step.  Default multi-GPU scaling is weak: every rank
+owns its own mesh (SURVEY.md §8e sample-DP).  Other configs (--workload): cfg1 = configs[0] (main.py
+widths, batch 4 x 4096), cfg3 = configs[2] (256k-point 3-D mesh, d=256, 8 experts), cfg4 = configs[3]
+(ONE 1M-point mesh point-sharded over the ranks: strong scaling), cfg5 = configs[4] (64 variable
+meshes, LPT sample-DP).  --points / --meshes shrink them to fit fewer GPUs.
 
 value = all query points processed by all ranks / max-over-ranks wall time of the K timed steps.
 roofline: the dominant kernel (fused MoE expert chains, backward) timed live with hipEvents on
@@ -56,6 +59,28 @@ WORKLOADS = {
                  N=10000, M=805, B=1,
                  desc="configs[1]: GNOT 4-layer, 4-expert, d=128, 8 heads, 2 input functions, "
                       "2-D irregular mesh 10k points/sample (805 points per input function), fp32 fwd+bwd"),
+    # BASELINE.json configs[2]: synthetic 3-D mesh, 256k points, d=256, 8 experts (the reference
+    # config is bf16; this path computes the reference's fp32)
+    "cfg3": dict(model=dict(input_dim=3, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=4,
+                            n_attn_hidden_dim=256, n_mlp_num_layers=4, n_mlp_hidden_dim=256,
+                            n_input_hidden_dim=256, n_expert=8, n_head=8, n_input_functions=1),
+                 N=262144, M=805, B=1,
+                 desc="configs[2]: synthetic 3-D mesh 262,144 points/sample, d=256, 8 experts, 8 heads, "
+                      "1 input function (805 points), fp32 fwd+bwd"),
+    # BASELINE.json configs[3]: ONE 1M-point mesh point-sharded over the ranks (strong scaling)
+    "cfg4": dict(model=dict(input_dim=3, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=4,
+                            n_attn_hidden_dim=256, n_mlp_num_layers=4, n_mlp_hidden_dim=256,
+                            n_input_hidden_dim=256, n_expert=8, n_head=8, n_input_functions=1),
+                 N=1048576, M=805, B=1, shard=True,
+                 desc="configs[3]: synthetic 3-D mesh of 1,048,576 points point-sharded over the GPUs "
+                      "(state all-reduce + scramble all-to-all over RCCL), d=256, 8 experts, fp32 fwd+bwd"),
+    # BASELINE.json configs[4]: 64 variable meshes (1k-50k points, packed), sample-DP with LPT balancing
+    "cfg5": dict(model=dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=4,
+                            n_attn_hidden_dim=256, n_mlp_num_layers=4, n_mlp_hidden_dim=256,
+                            n_input_hidden_dim=256, n_expert=3, n_head=8, n_input_functions=1),
+                 N=0, M=805, B=64, variable=(1000, 50000),
+                 desc="configs[4]: 64 meshes of U{1k..50k} points (seeded), packed offsets, sample-DP over the "
+                      "GPUs with longest-processing-time balancing, main.py widths, fp32 fwd+bwd"),
     # BASELINE.json configs[0] (main.py defaults, ~1-4k points/sample, batch 4)
     "cfg1": dict(model=dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=4,
                             n_attn_hidden_dim=256, n_mlp_num_layers=4, n_mlp_hidden_dim=256,
@@ -72,6 +97,47 @@ def rel_l2_loss(out, tgt, seg, B):
     num = torch.zeros(B, C, device=out.device).index_add_(0, seg, (out - tgt) ** 2)
     den = torch.zeros(B, C, device=out.device).index_add_(0, seg, tgt ** 2)
     return (num / den).sqrt().mean()
+
+
+def make_rank_batch(w, rank, world, device):
+    """This rank's share of the step's data, the loss normaliser and the step's total point count.
+    sample-DP: `B` meshes of `N` points per rank (seeded by rank); configs[4]: the rank's LPT share of
+    64 variable meshes; point-shard (configs[3]): the rank's slice of ONE mesh (every rank generates
+    the same global mesh and keeps its gnot_amd.parallel.shard_range)."""
+    from gnot_amd import parallel as par
+    m = w["model"]
+    if w.get("variable"):
+        g = torch.Generator(device="cpu").manual_seed(0)
+        lo, hi = w["variable"]
+        sizes = torch.randint(lo, hi + 1, (w["B"],), generator=g).tolist()
+        mine = par.lpt_partition(sizes, world)[rank]
+        xs, ys, fl, th = [], [], [], []
+        for b in mine:                                    # every mesh's data is seeded by its index
+            gb = torch.Generator(device="cpu").manual_seed(1000 + b)
+            xs.append(torch.rand(sizes[b], m["input_dim"], generator=gb))
+            th.append(torch.rand(1, m["theta_dim"], generator=gb))
+            fl.append([torch.rand(w["M"], m["input_func_dim"], generator=gb) for _ in range(m["n_input_functions"])])
+            ys.append(torch.randn(sizes[b], m["out_dim"], generator=gb))
+        Bl = len(mine)
+        x_off = [0]
+        for xb in xs:
+            x_off.append(x_off[-1] + xb.shape[0])
+        fns = [torch.cat([fl[k][i] for k in range(Bl)]) for i in range(m["n_input_functions"])]
+        fn_offs = [[k * w["M"] for k in range(Bl + 1)] for _ in range(m["n_input_functions"])]
+        seg = torch.repeat_interleave(torch.arange(Bl), torch.tensor([xb.shape[0] for xb in xs]))
+        to = lambda t: t.to(device)
+        return dict(x=to(torch.cat(xs)), x_off=x_off, theta=to(torch.cat(th)), fns=[to(f) for f in fns],
+                    fn_offs=fn_offs, y=to(torch.cat(ys)), seg=to(seg), B=Bl, norm=w["B"], n_global=None,
+                    step_points=sum(sizes))
+    if w.get("shard"):
+        x, x_off, theta, fns, fn_offs, y, seg = make_batch(w, 100, torch.device("cpu"))
+        lo, hi = par.shard_range(w["N"], rank, world)
+        to = lambda t: t.to(device)
+        return dict(x=to(x[lo:hi]), x_off=[0, hi - lo], theta=to(theta), fns=[to(f) for f in fns], fn_offs=fn_offs,
+                    y=to(y[lo:hi]), seg=to(seg[lo:hi]), B=1, norm=1, n_global=[w["N"]], step_points=w["N"])
+    x, x_off, theta, fns, fn_offs, y, seg = make_batch(w, 100 + rank, device)
+    return dict(x=x, x_off=x_off, theta=theta, fns=fns, fn_offs=fn_offs, y=y, seg=seg, B=w["B"],
+                norm=w["B"] * world, n_global=None, step_points=w["B"] * w["N"] * world)
 
 
 def make_batch(w, seed, device):
@@ -128,6 +194,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
     ap.add_argument("--points", type=int, default=0, help="override points per sample")
+    ap.add_argument("--meshes", type=int, default=0, help="cfg5: override the number of meshes")
     ap.add_argument("--roofline-kernel", default="moe_bwd", choices=["moe_fwd", "moe_bwd", "wgrad"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
@@ -147,32 +214,44 @@ def main():
     w = dict(WORKLOADS[args.workload])
     if args.points:
         w["N"] = args.points
+    if args.meshes:
+        w["B"] = args.meshes
     from gnot_amd import GNOT
     m = w["model"]
     torch.manual_seed(1234)                       # same initial weights on every rank
     model = GNOT(*[m[k] for k in ("input_dim", "theta_dim", "input_func_dim", "out_dim", "n_attn_layers",
                                   "n_attn_hidden_dim", "n_mlp_num_layers", "n_mlp_hidden_dim",
                                   "n_input_hidden_dim", "n_expert", "n_head", "n_input_functions")]).to(device)
-    use_graph = not args.no_graph
+    shard = bool(w.get("shard")) and world > 1
+    # the point-shard exchanges run inside the engine's launch sequence (RCCL through callbacks): eager
+    use_graph = not args.no_graph and not shard
     # main.py:50-51 AdamW(lr=1e-3), fused multi-tensor kernel; capturable keeps its step count on device
     opt = torch.optim.AdamW(model.parameters(), lr=1e-3, fused=True, capturable=use_graph)
-    x, x_off, theta, fns, fn_offs, y, seg = make_batch(w, 100 + rank, device)
-    B = w["B"]
+    D = make_rank_batch(w, rank, world, device)
+    x, x_off, theta, fns, fn_offs, y, seg, B = (D[k] for k in ("x", "x_off", "theta", "fns", "fn_offs", "y", "seg", "B"))
     eng = model.engine()
+    if shard:
+        from gnot_amd import parallel as par
+        model.set_point_shard(par.PointShardComm())
 
-    # one training step = [forward + RelL2 + backward] -> (N>1: ONE all-reduce of the flat gradient
-    # buffer, sample-DP) -> [AdamW].  With hipGraphs the two bracketed parts are captured once and
+    # one training step = [forward + RelL2 + backward] -> (N>1: ONE all-reduce (sum) of the flat
+    # gradient buffer) -> [AdamW].  With hipGraphs the two bracketed parts are captured once and
     # replayed; the collective stays an eager RCCL call between them.
     def fwd_bwd():
-        out = model.forward_packed(x, x_off, theta, fns, fn_offs)
-        loss = rel_l2_loss(out, y, seg, B)
+        out = model.forward_packed(x, x_off, theta, fns, fn_offs, n_global=D["n_global"])
+        if shard:
+            from gnot_amd import parallel as par
+            loss = par.rel_l2_loss_sharded(out, y, seg, B)
+        else:
+            # mean over ALL samples of the step (every rank's): local sum / global sample count
+            loss = rel_l2_loss(out, y, seg, B) * (B / D["norm"])
         opt.zero_grad(set_to_none=True)
         loss.backward()
         return loss
 
     def allreduce():
         if world > 1:
-            dist.all_reduce(eng.grad_flat, op=dist.ReduceOp.AVG)
+            dist.all_reduce(eng.grad_flat, op=dist.ReduceOp.SUM)
 
     def eager_step():
         fwd_bwd()
@@ -242,7 +321,7 @@ def main():
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    pts = B * w["N"] * args.steps * world
+    pts = D["step_points"] * args.steps
     avg_launch_ms = kms / max(klaunch, 1)
     achieved = (kflops / max(klaunch, 1)) / (avg_launch_ms * 1e-3) / 1e12 if klaunch and kms > 0 else 0.0
     result = {
@@ -254,16 +333,16 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if w.get("shard") else "weak",
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic: coords/theta/input-function rows U[0,1], targets N(0,1), seeded per rank; "
                 "random-init weights (torch.manual_seed)",
-        "config": {"workload": w["desc"], "points_per_gpu": B * w["N"], "samples_per_gpu": B,
+        "config": {"workload": w["desc"], "points_per_step": D["step_points"], "samples_per_gpu": B,
                    "input_function_points": w["M"], "hidden": m["n_attn_hidden_dim"], "experts": m["n_expert"],
                    "heads": m["n_head"], "blocks": m["n_attn_layers"], "mlp_layers": m["n_mlp_num_layers"],
                    "input_functions": m["n_input_functions"],
-                   "parallelism": f"sample-dp{world}" if world > 1 else "single",
+                   "parallelism": (f"point-shard{world}" if shard else f"sample-dp{world}") if world > 1 else "single",
                    "step": "pack+fwd+RelL2+bwd+AdamW" + (" (hipGraph replay)" if use_graph else " (eager)")},
         "roofline": {
             "kernel": {"moe_fwd": "chain_fwd_kernel (fused MoE expert chains, forward)",
@@ -280,7 +359,7 @@ def main():
             "launches": klaunch,
         },
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload in ("cfg1", "cfg2"):
         result["cpu_baseline"] = cpu_baseline(w)
     if rank == 0:
         print(json.dumps(result), flush=True)
