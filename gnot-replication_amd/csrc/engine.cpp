@@ -143,6 +143,7 @@ struct gnot_plan {
   // backward overlap: weight-gradient GEMMs run on a side stream; every buffer they read is
   // double-buffered and guarded by the event of its last side-stream reader
   hipStream_t side = nullptr;
+  hipStream_t side2 = nullptr;          // input-function branch, concurrent with the query branch
   std::vector<hipEvent_t> evs;
   size_t ev_next = 0;
   std::map<const float*, hipEvent_t> readers;
@@ -212,6 +213,8 @@ struct gnot_plan {
   int k_x() const { return 1 + 2 * L + I; }
   int k_gate() const { return 2 + 2 * L + I; }
   std::string dsum_buf(bool m1) const { return m1 ? "dsum1" : "dsum0"; }
+  // input-function encoder chains run on side2 with their own dZ buffer; the others alternate dz0/dz1
+  std::string dz_name(int kcall) const { return (kcall >= k_fn(0) && kcall < k_fn(0) + I) ? "dzf" : dz_buf(kcall); }
   std::string dqkv_buf(bool cross) const { return cross ? "dqkv1" : "dqkv0"; }
   std::string dkv_buf(int l, int i) const { return "dkv" + std::to_string(l) + "_" + std::to_string(i); }
   std::string dstate_fn(int l, int i) const { return "dstate" + std::to_string(l) + "_" + std::to_string(i); }
@@ -279,6 +282,7 @@ extern "C" void gnot_plan_destroy(gnot_plan* plan) {
   for (hipEvent_t e : plan->prof_events) (void)hipEventDestroy(e);
   for (hipEvent_t e : plan->evs) (void)hipEventDestroy(e);
   if (plan->side) (void)hipStreamDestroy(plan->side);
+  if (plan->side2) (void)hipStreamDestroy(plan->side2);
   delete plan;
 }
 
@@ -557,7 +561,7 @@ static void build_groups(gnot_plan* p) {
   // chain input (j = 0) or gelu(saved pre-activation j-1)
   auto chain_group = [&](WgradGroup& G, int kcall, const std::vector<int>& firsts, long rows, const float* x0,
                          long ldx0, const float* save) {
-    const float* dz = p->P_(p->dz_buf(kcall));
+    const float* dz = p->P_(p->dz_name(kcall));
     for (size_t c = 0; c < firsts.size(); ++c)
       for (int j = 0; j < NL; ++j) {
         const float* dzp = dz + ((long)c * NL + j) * rows * D;
@@ -987,7 +991,8 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
       C.add("dfn" + std::to_string(i), p->Q[i] * D, D);
     }
     C.add("dz0", E * NL * std::max(P, Qmax) * D, D);
-    C.add("dz1", E * NL * std::max(P, Qmax) * D, D);
+    C.add("dz1", E * NL * P * D, D);
+    if (I > 0) C.add("dzf", NL * Qmax * D, D);
   }
 
   // ---------------- device tables (host images; uploaded at bind)
@@ -1045,6 +1050,7 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
   tbl(p->kvbwd_jobs.size() * sizeof(AttnKVBwdArgs));
   for (auto& v : p->dfn_jobs) tbl(v.size() * sizeof(LinearArgs));
   C.add("slab_wgrad", p->slab_wgrad_floats, 0);
+  if (I > 0 && tr) C.add("slab_wgrad2", p->slab_wgrad_floats, 0);   // weight grads on side2
   C.add("slab_state", p->slab_state_floats, 0);
   const size_t table_off = C.raw(p->table_bytes);
   p->bufs["__tables"] = Buf{table_off, 0, nullptr};
@@ -1168,8 +1174,18 @@ extern "C" int gnot_plan_bind_workspace(gnot_plan* p, void* workspace, size_t by
   p->d_xrecv_prefix = static_cast<int*>(put(p->xrecv_prefix.data(), p->xrecv_prefix.size() * sizeof(int)));
   if (cur > p->table_bytes) return fail(GNOT_E_INVALID, "internal: table overflow");
   GNOT_CK(hipMemcpy(tp, host.data(), cur, hipMemcpyHostToDevice));
-  if (p->training && !p->side) GNOT_CK(hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking));
-  while (p->training && p->evs.size() < 256) {
+  if (!p->side2) GNOT_CK(hipStreamCreateWithFlags(&p->side2, hipStreamNonBlocking));
+  if (!p->side) {
+    // same priority as the caller's stream: measured on MI355X, a low- (or high-) priority side
+    // stream serialises against the main one and the step takes ~1.9x longer (GNOT_SIDE_PRIO)
+    int least = 0, greatest = 0;
+    GNOT_CK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    const char* env = std::getenv("GNOT_SIDE_PRIO");
+    const int prio = env ? std::atoi(env) : 0;
+    if (std::getenv("GNOT_DEBUG_PRIO")) std::fprintf(stderr, "[gnot] stream priority range least=%d greatest=%d, side=%d\n", least, greatest, prio);
+    GNOT_CK(hipStreamCreateWithPriority(&p->side, hipStreamNonBlocking, prio));
+  }
+  while (p->evs.size() < 256) {
     hipEvent_t e;
     GNOT_CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     p->evs.push_back(e);
@@ -1291,10 +1307,14 @@ int run_wgrad_side(Ctx& c, const WgradGroup& G, std::initializer_list<const floa
   if (G.jobs.empty()) return GNOT_OK;
   gnot_plan* p = c.p;
   static const bool serial = std::getenv("GNOT_SERIAL_WGRAD") != nullptr;   // diagnostics: no overlap
-  if (serial) {
+  // only the caller's stream forks to the side stream (a fork from another forked stream is not
+  // captured correctly into a hipGraph on ROCm 7: capture_end faults); other streams run their
+  // weight gradients in order on themselves, using their own slab
+  if (serial || c.s == p->side2) {
+    float* slab = c.s == p->side2 ? p->P_("slab_wgrad2") : p->P_("slab_wgrad");
     ProfScope ps(c, "wgrad", group_flops(G));
     GNOT_CK(launch_wgrad(G.d_jobs, G.d_wg_prefix, (int)G.jobs.size(), G.total_wgs, G.d_red_prefix,
-                         G.total_red, p->P_("slab_wgrad"), c.s));
+                         G.total_red, slab, c.s));
     return GNOT_OK;
   }
   hipEvent_t fork = next_event(p);
@@ -1462,6 +1482,33 @@ extern "C" int gnot_forward(gnot_plan* p, const float* x, const float* theta, co
       GNOT_CK(hipMemcpy2DAsync(p->P_(n), p->bufs[n].ld * 4, fns[i], p->F * 4, p->F * 4, p->Q[i],
                                hipMemcpyDeviceToDevice, c.s));
   }
+  // the input-function branch (encoders, every block's K/V projections and states) depends only on
+  // the input functions: it runs on side2 while the query branch (gating, x encoder) runs here
+  static const bool no_fwd2 = std::getenv("GNOT_NO_SIDE2_FWD") != nullptr;
+  const bool br = p->I > 0 && !no_fwd2;
+  Ctx cf{p, br ? p->side2 : c.s};
+  if (br) {
+    hipEvent_t fork = next_event(p);
+    GNOT_CK(hipEventRecord(fork, c.s));
+    GNOT_CK(hipStreamWaitEvent(cf.s, fork, 0));
+  }
+  // input-function encoders (model.py:164-166)
+  for (int i = 0; i < p->I; ++i) {
+    const std::string si = std::to_string(i);
+    ChainArgs a = chain_args(p, p->ch_fn[i], p->Q[i]);
+    a.X = p->P_("fn" + si); a.ldx = p->bufs["fn" + si].ld;
+    a.Y = p->P_("fnenc" + si); a.ldy = D; a.mode = CH_STORE;
+    if (tr) { a.save = p->P_("fn_save" + si); a.save_layer_stride = p->Q[i] * D; a.save_chain_stride = NL * p->Q[i] * D; }
+    GNOT_CK(launch_chain_fwd(a, cf.s));
+  }
+  // key/value projections (model.py:67-75) and states (model.py:77-79) of every (block, input
+  // function): they depend only on the input-function encodings, so all L*I of them run batched here
+  if (p->I > 0 && p->L > 0) {
+    long Qmax = 0;
+    for (long q : p->Q) Qmax = std::max(Qmax, q);
+    GNOT_CK(launch_linear_batch(p->d_fwd_kv_jobs, (int)p->fwd_kv_jobs.size(), (int)Qmax, 2 * D, D, cf.s));
+    GNOT_RUN(run_state(cf, p->st_fn));
+  }
   GNOT_CK(launch_concat_theta(p->P_("x"), p->bufs["x"].ld, p->in, p->P_("theta"), p->th, p->d_xoff, p->B,
                               p->P_("xin"), p->bufs["xin"].ld, (int)P, c.s));
   // gating (model.py:155-156)
@@ -1480,22 +1527,10 @@ extern "C" int gnot_forward(gnot_plan* p, const float* x, const float* theta, co
     if (tr) { a.save = p->P_("x_save"); a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D; }
     GNOT_CK(launch_chain_fwd(a, c.s));
   }
-  // input-function encoders (model.py:164-166)
-  for (int i = 0; i < p->I; ++i) {
-    const std::string si = std::to_string(i);
-    ChainArgs a = chain_args(p, p->ch_fn[i], p->Q[i]);
-    a.X = p->P_("fn" + si); a.ldx = p->bufs["fn" + si].ld;
-    a.Y = p->P_("fnenc" + si); a.ldy = D; a.mode = CH_STORE;
-    if (tr) { a.save = p->P_("fn_save" + si); a.save_layer_stride = p->Q[i] * D; a.save_chain_stride = NL * p->Q[i] * D; }
-    GNOT_CK(launch_chain_fwd(a, c.s));
-  }
-  // key/value projections (model.py:67-75) and states (model.py:77-79) of every (block, input
-  // function): they depend only on the input-function encodings, so all L*I of them run batched here
-  if (p->I > 0 && p->L > 0) {
-    long Qmax = 0;
-    for (long q : p->Q) Qmax = std::max(Qmax, q);
-    GNOT_CK(launch_linear_batch(p->d_fwd_kv_jobs, (int)p->fwd_kv_jobs.size(), (int)Qmax, 2 * D, D, c.s));
-    GNOT_RUN(run_state(c, p->st_fn));
+  if (br) {                                // join the input-function branch
+    hipEvent_t join = next_event(p);
+    GNOT_CK(hipEventRecord(join, cf.s));
+    GNOT_CK(hipStreamWaitEvent(c.s, join, 0));
   }
   // blocks (model.py:126-139)
   for (int l = 0; l < p->L; ++l) {
@@ -1552,15 +1587,18 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
   GNOT_CK(hipMemsetAsync(p->P_("dscore"), 0, P * p->bufs["dscore"].ld * 4, c.s));
   // one chain backward: dZ of every Linear into the chain call's dz slot, then its weight gradients
   // are forked to the side stream
-  auto chain_bwd = [&](ChainArgs& a, int kcall, long rows, const WgradGroup& G, const char* prof) -> int {
-    float* dz = p->P_(p->dz_buf(kcall));
-    GNOT_RUN(guard_write(c, dz));
+  auto chain_bwd_on = [&](Ctx& cc, ChainArgs& a, int kcall, long rows, const WgradGroup& G, const char* prof) -> int {
+    float* dz = p->P_(p->dz_name(kcall));
+    GNOT_RUN(guard_write(cc, dz));
     a.dz = dz; a.dz_layer_stride = rows * D; a.dz_chain_stride = NL * rows * D;
     {
-      ProfScope ps(c, prof, 2.0 * a.nchains * rows * NL * (double)D * D);
-      GNOT_CK(launch_chain_bwd(a, c.s));
+      ProfScope ps(cc, prof, 2.0 * a.nchains * rows * NL * (double)D * D);
+      GNOT_CK(launch_chain_bwd(a, cc.s));
     }
-    return run_wgrad_side(c, G, {dz});
+    return run_wgrad_side(cc, G, {dz});
+  };
+  auto chain_bwd = [&](ChainArgs& a, int kcall, long rows, const WgradGroup& G, const char* prof) -> int {
+    return chain_bwd_on(c, a, kcall, rows, G, prof);
   };
   // decoder (model.py:171)
   {
@@ -1588,6 +1626,15 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
       GNOT_RUN(attn_backward(c, l, m1));
     }
   }
+  // the input-function branch again runs on side2, concurrently with the query encoder and gating
+  static const bool no_bwd2 = std::getenv("GNOT_NO_SIDE2_BWD") != nullptr;
+  const bool br = p->I > 0 && !no_bwd2;
+  Ctx cf{p, br ? p->side2 : c.s};
+  if (br) {
+    hipEvent_t fork = next_event(p);
+    GNOT_CK(hipEventRecord(fork, c.s));
+    GNOT_CK(hipStreamWaitEvent(cf.s, fork, 0));
+  }
   // dK, dV of every (block, input function), the encodings' gradient and the key/value weight
   // gradients, batched over blocks
   if (p->I > 0 && p->L > 0) {
@@ -1597,21 +1644,21 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
       Qmax = std::max(Qmax, p->Q[i]);
       maxch = std::max(maxch, (int)p->fchunks[i].size());
     }
-    GNOT_CK(launch_attn_kv_bwd_batch(p->d_kvbwd_jobs, (int)p->kvbwd_jobs.size(), maxch, p->H, p->dh, c.s));
+    GNOT_CK(launch_attn_kv_bwd_batch(p->d_kvbwd_jobs, (int)p->kvbwd_jobs.size(), maxch, p->H, p->dh, cf.s));
     for (size_t k = 0; k < p->d_dfn_jobs.size(); ++k)
-      GNOT_CK(launch_linear_batch(p->d_dfn_jobs[k], p->I, (int)Qmax, D, D, c.s));
-    GNOT_RUN(run_wgrad_side(c, p->wg_fnkv, {}));
+      GNOT_CK(launch_linear_batch(p->d_dfn_jobs[k], p->I, (int)Qmax, D, D, cf.s));
+    GNOT_RUN(run_wgrad_side(cf, p->wg_fnkv, {}));
   }
   if (p->I > 0 && p->L == 0)   // encodings unused by the output: zero gradients
     for (int i = 0; i < p->I; ++i)
-      GNOT_CK(hipMemsetAsync(p->P_("dfn" + std::to_string(i)), 0, p->Q[i] * D * 4, c.s));
+      GNOT_CK(hipMemsetAsync(p->P_("dfn" + std::to_string(i)), 0, p->Q[i] * D * 4, cf.s));
   // input-function encoders (their inputs need no gradient)
   for (int i = 0; i < p->I; ++i) {
     const std::string si = std::to_string(i);
     ChainArgs a = chain_args(p, p->ch_fn[i], p->Q[i]);
     a.dY = p->P_("dfn" + si); a.lddy = D; a.mode = CH_STORE;
     a.save = p->P_("fn_save" + si); a.save_layer_stride = p->Q[i] * D; a.save_chain_stride = NL * p->Q[i] * D;
-    GNOT_RUN(chain_bwd(a, p->k_fn(i), p->Q[i], p->wg_fn[i], "chain_bwd"));
+    GNOT_RUN(chain_bwd_on(cf, a, p->k_fn(i), p->Q[i], p->wg_fn[i], "chain_bwd"));
   }
   // query encoder
   {
@@ -1627,6 +1674,11 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
     a.dscore = p->P_("dscore");
     a.save = p->P_("gate_save"); a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D;
     GNOT_RUN(chain_bwd(a, p->k_gate(), P, p->wg_gate, "chain_bwd"));
+  }
+  if (br) {                                // join the input-function branch
+    hipEvent_t joinf = next_event(p);
+    GNOT_CK(hipEventRecord(joinf, cf.s));
+    GNOT_CK(hipStreamWaitEvent(c.s, joinf, 0));
   }
   // join the side stream: every gradient is complete when the caller's stream moves on
   hipEvent_t join = next_event(p);
