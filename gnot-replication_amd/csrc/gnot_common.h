@@ -218,7 +218,7 @@ GNOT_DEV void mm_tiles_pipe(const float4* __restrict__ Wg, const float4* __restr
     float4* nb = lds + ((cnt + 1) & 1) * kChunkF4;
     if (c + 1 < NC) stage_image(nb, Wg + (c + 1) * CH4, CH4, nwaves, wave, lane);
     else if (next_W) stage_image(nb, next_W, next_f4, nwaves, wave, lane);
-    if (c + 1 == NC) hook();                           // e.g. prefetch the next layer's saved rows
+    if (c == 0) hook();   // e.g. prefetch the next layer's saved rows: a whole layer of MFMAs to land
     const float4* cb = lds + (cnt & 1) * kChunkF4;
     float4 wc[OCH], wn[OCH];
 #pragma unroll

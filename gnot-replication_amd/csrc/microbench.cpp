@@ -1,0 +1,131 @@
+// Kernel microbenchmark (diagnostics, not part of libgnot_hip.so): times the internal launchers on
+// synthetic cfg2-sized operands with hipEvents, one kernel class at a time, no contention.
+//   make microbench && ./microbench [points] [D]
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <algorithm>
+#include <cstdlib>
+#include <vector>
+
+#include "gnot_kernels.h"
+
+using namespace gnot;
+
+#define CK(x)                                                                                   \
+  do {                                                                                          \
+    hipError_t e_ = (x);                                                                        \
+    if (e_ != hipSuccess) {                                                                     \
+      std::fprintf(stderr, "%s:%d %s -> %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+      std::exit(1);                                                                             \
+    }                                                                                           \
+  } while (0)
+
+static float* dalloc(size_t n, float scale) {
+  std::vector<float> h(n);
+  for (size_t i = 0; i < n; ++i) h[i] = scale * ((float)((i * 2654435761u) % 2001) / 1000.0f - 1.0f);
+  float* d = nullptr;
+  CK(hipMalloc(&d, n * sizeof(float)));
+  CK(hipMemcpy(d, h.data(), n * sizeof(float), hipMemcpyHostToDevice));
+  return d;
+}
+
+template <typename F>
+static double time_us(F&& f, int reps = 50) {
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  for (int i = 0; i < 5; ++i) f();
+  CK(hipEventRecord(a, nullptr));
+  for (int i = 0; i < reps; ++i) f();
+  CK(hipEventRecord(b, nullptr));
+  CK(hipEventSynchronize(b));
+  float ms = 0.f;
+  CK(hipEventElapsedTime(&ms, a, b));
+  return ms * 1e3 / reps;
+}
+
+int main(int argc, char** argv) {
+  const int P = argc > 1 ? std::atoi(argv[1]) : 10000;
+  const int D = argc > 2 ? std::atoi(argv[2]) : 128;
+  const int E = 4, NL = 5, DT = D / 16;
+  // packed weight images: NL layers x E chains, fwd and transposed (values arbitrary, finite)
+  const size_t img4 = (size_t)DT * DT * 64;     // float4 per DxD image
+  float4* W = reinterpret_cast<float4*>(dalloc(img4 * 4 * NL * E * 2, 0.05f));
+  float* bias = dalloc((size_t)NL * E * D, 0.01f);
+  std::vector<ChainLayer> layers;
+  for (int e = 0; e < E; ++e)
+    for (int j = 0; j < NL; ++j) {
+      const size_t k = (size_t)e * NL + j;
+      layers.push_back(ChainLayer{W + 2 * k * img4, W + (2 * k + 1) * img4, bias + k * D});
+    }
+  ChainLayer* dlayers = nullptr;
+  CK(hipMalloc(&dlayers, layers.size() * sizeof(ChainLayer)));
+  CK(hipMemcpy(dlayers, layers.data(), layers.size() * sizeof(ChainLayer), hipMemcpyHostToDevice));
+  float* X = dalloc((size_t)P * D, 1.0f);
+  float* Y = dalloc((size_t)E * P * D, 0.0f);
+  float* save = dalloc((size_t)E * NL * P * D, 1.0f);
+  float* dz = dalloc((size_t)E * NL * P * D, 0.0f);
+  float* scores = dalloc((size_t)P * 4, 0.25f);
+  float* dscore = dalloc((size_t)P * 4, 0.0f);
+  float* dX = dalloc((size_t)E * P * D, 0.0f);
+
+  ChainArgs a{};
+  a.D = D; a.KT0 = DT; a.OTL = DT; a.nlin = NL; a.in_dim = D; a.out_dim = D; a.P = P; a.nchains = E;
+  a.layers = dlayers; a.X = X; a.ldx = D; a.Y = Y; a.ldy = D; a.y_chain_stride = (long)P * D;
+  a.scores = scores; a.ldsc = 4; a.mode = CH_MOE;
+  a.save = save; a.save_layer_stride = (long)P * D; a.save_chain_stride = (long)NL * P * D;
+  const double fl = 2.0 * E * P * NL * (double)D * D;
+  double t = time_us([&] { CK(launch_chain_fwd(a, nullptr)); });
+  std::printf("chain_fwd  MoE E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
+  ChainArgs bw = a;
+  bw.dY = X; bw.lddy = D; bw.dscore = dscore; bw.dz = dz; bw.dz_layer_stride = (long)P * D;
+  bw.dz_chain_stride = (long)NL * P * D; bw.dX = dX; bw.lddx = D; bw.dx_chain_stride = (long)P * D;
+  t = time_us([&] { CK(launch_chain_bwd(bw, nullptr)); });
+  std::printf("chain_bwd  MoE E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
+
+  for (int NO : {D, 3 * D}) {
+    LinearArgs l{};
+    l.nseg = 1; l.X[0] = X; l.Wp[0] = W; l.ldx = D; l.nsum = 1; l.K = D; l.bias = bias; l.Y = Y; l.ldy = NO;
+    l.NO = NO; l.P = P; l.epi = EPI_STORE; l.nsoft = 0; l.dh = 16;
+    t = time_us([&] { CK(launch_linear(l, D, nullptr)); });
+    std::printf("linear     P=%d K=%d NO=%d: %8.2f us  %6.1f TFLOP/s\n", P, D, NO, t, 2.0 * P * D * NO / t / 1e6);
+  }
+  // weight-gradient point-reduction GEMM of one MoE chain group: E*NL jobs of D x D over P points,
+  // split-K exactly as the engine sizes it (<= 512 workgroups, >= 128 points per split)
+  {
+    std::vector<WgradJob> jobs;
+    std::vector<int> wg_pre, red_pre;
+    int wg = 0, red = 0;
+    long slab_off = 0;
+    float* dW = dalloc((size_t)E * NL * (D * D + D), 0.f);
+    const int njobs = E * NL;
+    const int tiles = ((D + 127) / 128) * ((D + 127) / 128);
+    const long want = std::max<long>(1, 512 / ((long)njobs * tiles));
+    for (int k = 0; k < njobs; ++k) {
+      WgradJob J{};
+      J.dz = dz + (size_t)k * P * D; J.lddz = D; J.x = save + (size_t)k * P * D; J.ldx = D; J.x_gelu = 1;
+      J.out = D; J.in = D; J.dW = dW + (size_t)k * (D * D + D); J.db = J.dW + D * D; J.P = P;
+      J.tiles_o = (D + 127) / 128; J.tiles_i = J.tiles_o;
+      J.splits = (int)std::min<long>(std::min<long>(want, std::max<long>(1, P / 128)), 256);
+      J.slab_off = slab_off;
+      slab_off += (long)J.splits * tiles * 128 * 129;
+      wg_pre.push_back(wg); wg += tiles * J.splits;
+      red_pre.push_back(red); red += tiles * 128 * 129;
+      jobs.push_back(J);
+    }
+    WgradJob* djobs = nullptr;
+    int* dpre = nullptr;
+    CK(hipMalloc(&djobs, jobs.size() * sizeof(WgradJob)));
+    CK(hipMemcpy(djobs, jobs.data(), jobs.size() * sizeof(WgradJob), hipMemcpyHostToDevice));
+    std::vector<int> pre(wg_pre);
+    pre.insert(pre.end(), red_pre.begin(), red_pre.end());
+    CK(hipMalloc(&dpre, pre.size() * sizeof(int)));
+    CK(hipMemcpy(dpre, pre.data(), pre.size() * sizeof(int), hipMemcpyHostToDevice));
+    float* slab = dalloc((size_t)slab_off, 0.f);
+    t = time_us([&] { CK(launch_wgrad(djobs, dpre, njobs, wg, dpre + njobs, red, slab, nullptr)); }, 20);
+    std::printf("wgrad MoE  %d jobs P=%d D=%d (%d WGs): %8.2f us  %6.1f TFLOP/s\n", njobs, P, D, wg, t, fl / t / 1e6);
+  }
+  CK(hipDeviceSynchronize());
+  return 0;
+}

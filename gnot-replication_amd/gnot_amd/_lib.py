@@ -88,10 +88,11 @@ def load():
     """Load libgnot_hip.so (raises if it is missing: there is no CPU fallback)."""
     global _LIB
     if _LIB is None:
-        if not os.path.exists(LIB_PATH):
-            raise ImportError(f"{LIB_PATH} not found: build it with `make -C {CSRC}` "
+        path = os.environ.get("GNOT_LIB", LIB_PATH)      # experiment builds of the same library
+        if not os.path.exists(path):
+            raise ImportError(f"{path} not found: build it with `make -C {CSRC}` "
                               "(gnot_amd has no CPU fallback)")
-        _LIB = _declare(ctypes.CDLL(LIB_PATH))
+        _LIB = _declare(ctypes.CDLL(path))
     return _LIB
 
 
