@@ -198,6 +198,7 @@ def main():
     ap.add_argument("--roofline-kernel", default="moe_bwd", choices=["moe_fwd", "moe_bwd", "wgrad"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
+    ap.add_argument("--torch-adamw", action="store_true", help="torch's fused AdamW instead of the native one")
     ap.add_argument("--breakdown", action="store_true", help="print per-kernel-class device time to stderr")
     args = ap.parse_args()
 
@@ -225,11 +226,18 @@ def main():
     shard = bool(w.get("shard")) and world > 1
     # the point-shard exchanges run inside the engine's launch sequence (RCCL through callbacks): eager
     use_graph = not args.no_graph and not shard
-    # main.py:50-51 AdamW(lr=1e-3), fused multi-tensor kernel; capturable keeps its step count on device
-    opt = torch.optim.AdamW(model.parameters(), lr=1e-3, fused=True, capturable=use_graph)
+    from gnot_amd import train as gtrain
+    # main.py:50-51 AdamW(lr=1e-3): one native update over the flat parameter arena (gnot_adamw_step),
+    # or torch's fused multi-tensor AdamW (--torch-adamw; capturable keeps its step count on device)
+    if args.torch_adamw:
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-3, fused=True, capturable=use_graph)
+    else:
+        opt = gtrain.FlatAdamW(gtrain.flatten_parameters(model), lr=1e-3)
+    loss_fn = gtrain.RelL2Loss()
     D = make_rank_batch(w, rank, world, device)
     x, x_off, theta, fns, fn_offs, y, seg, B = (D[k] for k in ("x", "x_off", "theta", "fns", "fn_offs", "y", "seg", "B"))
     eng = model.engine()
+    eng.param_grads = bool(args.torch_adamw)      # the native AdamW reads the gradient arena directly
     if shard:
         from gnot_amd import parallel as par
         model.set_point_shard(par.PointShardComm())
@@ -243,11 +251,18 @@ def main():
             from gnot_amd import parallel as par
             loss = par.rel_l2_loss_sharded(out, y, seg, B)
         else:
-            # mean over ALL samples of the step (every rank's): local sum / global sample count
-            loss = rel_l2_loss(out, y, seg, B) * (B / D["norm"])
-        opt.zero_grad(set_to_none=True)
+            # native RelL2 (loss.py:14-23); mean over ALL samples of the step: local sum / global count
+            loss = loss_fn(x_off, out, y) * (B / D["norm"])
+        if args.torch_adamw:
+            opt.zero_grad(set_to_none=True)
         loss.backward()
         return loss
+
+    def opt_step():
+        if args.torch_adamw:
+            opt.step()
+        else:
+            opt.launch(eng.grad_flat)
 
     def allreduce():
         if world > 1:
@@ -256,7 +271,9 @@ def main():
     def eager_step():
         fwd_bwd()
         allreduce()
-        opt.step()
+        if not args.torch_adamw:
+            opt.prepare()
+        opt_step()
 
     # warm-up (also the capture warm-up: allocations, plan binding, optimizer state)
     side = torch.cuda.Stream(device)
@@ -289,12 +306,14 @@ def main():
         with torch.cuda.graph(g_fb):
             fwd_bwd()
         with torch.cuda.graph(g_opt, pool=g_fb.pool()):
-            opt.step()
+            opt_step()
         torch.cuda.synchronize()
 
         def graph_step():
             g_fb.replay()
             allreduce()
+            if not args.torch_adamw:
+                opt.prepare()         # this step's AdamW hyper-parameters -> device (outside the graph)
             g_opt.replay()
         step = graph_step
         for _ in range(2):
@@ -343,7 +362,7 @@ def main():
                    "heads": m["n_head"], "blocks": m["n_attn_layers"], "mlp_layers": m["n_mlp_num_layers"],
                    "input_functions": m["n_input_functions"],
                    "parallelism": (f"point-shard{world}" if shard else f"sample-dp{world}") if world > 1 else "single",
-                   "step": "pack+fwd+RelL2+bwd+AdamW" + (" (hipGraph replay)" if use_graph else " (eager)")},
+                   "step": "pack+fwd+RelL2+bwd+AdamW (native loss, " + ("torch fused AdamW" if args.torch_adamw else "native flat AdamW") + ")" + (" (hipGraph replay)" if use_graph else " (eager)")},
         "roofline": {
             "kernel": {"moe_fwd": "chain_fwd_kernel (fused MoE expert chains, forward)",
                        "moe_bwd": "chain_bwd_kernel (fused MoE expert chains, backward)",

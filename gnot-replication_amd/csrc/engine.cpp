@@ -1724,5 +1724,32 @@ extern "C" int gnot_debug_buffer(const gnot_plan* p, const char* name, float** p
   return GNOT_OK;
 }
 
+// ====================================================================== training step
+extern "C" size_t gnot_rel_l2_work_floats(const int64_t* off_host, int B, int C) {
+  if (!off_host || B <= 0 || C <= 0) return 0;
+  std::vector<long> off(off_host, off_host + B + 1);
+  return (size_t)B * rel_l2_splits(off.data(), B) * 2 * C + (size_t)B * C;
+}
+
+extern "C" int gnot_rel_l2_loss(const float* pred, const float* tgt, const int64_t* off_dev, const int64_t* off_host,
+                                int B, int C, float* work, float* loss, float* dpred, void* stream) {
+  if (!pred || !tgt || !off_dev || !off_host || B <= 0 || C <= 0 || !work || !loss)
+    return fail(GNOT_E_INVALID, "bad rel_l2 arguments");
+  std::vector<long> off(off_host, off_host + B + 1);
+  if (off[0] != 0) return fail(GNOT_E_INVALID, "off[0] must be 0");
+  for (int b = 0; b < B; ++b)
+    if (off[b + 1] < off[b]) return fail(GNOT_E_INVALID, "offsets must be non-decreasing");
+  GNOT_CK(launch_rel_l2(pred, tgt, reinterpret_cast<const long*>(off_dev), B, C, rel_l2_splits(off.data(), B),
+                        off[B], work, loss, dpred, static_cast<hipStream_t>(stream)));
+  return GNOT_OK;
+}
+
+extern "C" int gnot_adamw_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n,
+                               const float* hyper, void* stream) {
+  if (!param || !grad || !exp_avg || !exp_avg_sq || n < 0 || !hyper) return fail(GNOT_E_INVALID, "bad adamw arguments");
+  GNOT_CK(launch_adamw(param, grad, exp_avg, exp_avg_sq, n, hyper, static_cast<hipStream_t>(stream)));
+  return GNOT_OK;
+}
+
 extern "C" const char* gnot_last_error(void) { return g_err.c_str(); }
 extern "C" const char* gnot_version(void) { return "gnot-mi355x 0.1 (gfx950, fp32 MFMA)"; }

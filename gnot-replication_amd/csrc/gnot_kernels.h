@@ -154,4 +154,12 @@ struct CopySeg {
 hipError_t launch_segcopy(const CopySeg* segs, const int* prefix4, int nseg, int total4, const float* src, float* dst,
                           bool reverse, hipStream_t s);
 
+// ------------------------------------------------------------------ training step (train.hip)
+int rel_l2_splits(const long* off_host, int B);
+// work: B*nsplit*2C + B*C floats
+hipError_t launch_rel_l2(const float* pred, const float* tgt, const long* off_dev, int B, int C, int nsplit,
+                         long rows, float* work, float* loss, float* dpred, hipStream_t s);
+hipError_t launch_adamw(float* param, const float* grad, float* m, float* v, long n, const float* hyper,
+                        hipStream_t s);
+
 }  // namespace gnot

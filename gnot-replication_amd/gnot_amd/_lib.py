@@ -28,6 +28,7 @@ EXPORTS = [
     "gnot_plan_bind_workspace", "gnot_plan_grad_offsets", "gnot_pack_weights", "gnot_forward",
     "gnot_backward", "gnot_profile_enable", "gnot_profile_read", "gnot_debug_buffer", "gnot_last_error",
     "gnot_version", "gnot_plan_set_shard", "gnot_shard_range", "gnot_shard_exchange",
+    "gnot_rel_l2_work_floats", "gnot_rel_l2_loss", "gnot_adamw_step",
 ]
 
 # gnot_comm callbacks (include/gnot_hip.h)
@@ -74,6 +75,10 @@ def _declare(lib):
     lib.gnot_shard_range.argtypes = [i64, i32, i32, ctypes.POINTER(i64), ctypes.POINTER(i64)]
     lib.gnot_shard_exchange.argtypes = [i32, ctypes.POINTER(i64), i32, i32, i32, i32, ctypes.POINTER(i64),
                                         ctypes.POINTER(i64), ctypes.POINTER(i64), i64, ctypes.POINTER(i64)]
+    lib.gnot_rel_l2_work_floats.argtypes = [ctypes.POINTER(i64), i32, i32]
+    lib.gnot_rel_l2_work_floats.restype = sz
+    lib.gnot_rel_l2_loss.argtypes = [P, P, P, ctypes.POINTER(i64), i32, i32, P, P, P, P]
+    lib.gnot_adamw_step.argtypes = [P, P, P, P, i64, P, P]
     lib.gnot_last_error.restype = ctypes.c_char_p
     lib.gnot_last_error.argtypes = []
     lib.gnot_version.restype = ctypes.c_char_p

@@ -39,6 +39,7 @@ class Engine:
         self.grad_arena = None     # flat fp32 view of every parameter gradient (one buffer)
         self.grad_hook = None      # optional callable(grad_arena) run after the backward kernels
         self.grad_flat = None      # the flat copy of the arena handed to autograd by the last backward
+        self.param_grads = True    # False: no .grad tensors; grad_flat IS the arena (FlatAdamW reads it)
         self.comm = None           # parallel.PointShardComm when points are sharded over ranks
         self.fwd_token = 0
 

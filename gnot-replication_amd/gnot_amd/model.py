@@ -98,6 +98,11 @@ class _GNOTFunction(torch.autograd.Function):
             raise RuntimeError("gnot_amd keeps the activations of the most recent forward only; "
                                "backward must follow its own forward")
         eng.backward(dout.contiguous().float())
+        if not eng.param_grads:
+            # the caller consumes the arena itself (gnot_amd.train.FlatAdamW) before the next backward:
+            # no copy, and autograd accumulates nothing into .grad
+            eng.grad_flat = eng.grad_arena
+            return (None, None, None, None, None) + (None,) * ctx.nparams
         # ONE copy of the whole gradient arena (the workspace is reused by the next step); every
         # parameter gradient is a view of that fresh buffer
         flat = eng.grad_arena.clone()

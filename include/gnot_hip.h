@@ -136,6 +136,25 @@ int gnot_shard_range(int64_t n, int rank, int world, int64_t* lo, int64_t* hi);
 int gnot_shard_exchange(int B, const int64_t* n_global, int n_head, int head_dim, int rank, int world,
                         int64_t* send_counts, int64_t* recv_counts, int64_t* segs, int64_t cap, int64_t* nseg);
 
+/* ---------------------------------------------------------------- the training step around the path
+ * (stateless, stream-ordered, no allocation)
+ *
+ * RelL2Loss (reference loss.py:14-23, the dgl SumPooling of main.py:87-98 as packed segment sums):
+ * pred/tgt [rows, C] fp32 packed by the device offsets off_dev[B+1] (off_host = the same on the host,
+ * for sizing); writes the scalar loss = mean over (sample, channel) of sqrt(sum (p-t)^2 / sum t^2)
+ * to *loss (device) and, if dpred != NULL, d loss / d pred.  work: device scratch of
+ * gnot_rel_l2_work_floats(off_host, B, C) floats.  Deterministic (fixed-order reductions). */
+size_t gnot_rel_l2_work_floats(const int64_t* off_host, int B, int C);
+int gnot_rel_l2_loss(const float* pred, const float* tgt, const int64_t* off_dev, const int64_t* off_host, int B,
+                     int C, float* work, float* loss, float* dpred, void* stream);
+
+/* One torch.optim.AdamW step (main.py:51) over flat fp32 arrays of n elements (param, grad, exp_avg,
+ * exp_avg_sq), in torch's operation order.  hyper: DEVICE array of 8 floats {lr, beta1, beta2, eps,
+ * weight_decay, 1 - beta1^t, 1 - beta2^t, grad_scale}, so a captured graph picks up the schedule the
+ * host writes there (OneCycleLR changes lr and beta1, main.py:52). */
+int gnot_adamw_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, int64_t n, const float* hyper,
+                    void* stream);
+
 /* Live kernel timing for the bench's roofline: while enabled, every launch of kernel class `kind`
  * ("moe_fwd" fused expert chains forward, "moe_bwd" their backward, "wgrad" weight-gradient GEMMs;
  * "" disables) is bracketed by hipEvents on its stream.  gnot_profile_read synchronizes on those
