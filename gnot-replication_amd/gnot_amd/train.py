@@ -166,3 +166,72 @@ class FlatAdamW:
     def step(self, grad):
         self.prepare()
         self.launch(grad)
+
+
+# ------------------------------------------------------------------ driver (main.py:55-153)
+def save_checkpoint(model, path):
+    """torch.save(model.state_dict()) exactly as main.py:151 (reference-compatible keys/shapes)."""
+    torch.save(model.state_dict(), path)
+
+
+def load_checkpoint(model, path):
+    """Load a reference (or gnot_amd) state_dict checkpoint; tensors only (weights_only=True)."""
+    model.load_state_dict(torch.load(path, map_location="cpu", weights_only=True))
+    return model
+
+
+def _to(batch, dev):
+    return (batch["x"].to(dev), batch["x_off"], batch["theta"].to(dev), [f.to(dev) for f in batch["fns"]],
+            batch["fn_offs"], batch["y"].to(dev))
+
+
+def evaluate(model, loader, loss_fn=None):
+    """main.py:108-147: mean RelL2 over the test batches, no_grad (no activations kept)."""
+    loss_fn = loss_fn or RelL2Loss()
+    dev = next(model.parameters()).device
+    vals = []
+    with torch.no_grad():
+        for batch in loader:
+            x, x_off, theta, fns, fn_offs, y = _to(batch, dev)
+            out = model.forward_packed(x, x_off, theta, fns, fn_offs)
+            vals.append(float(loss_fn(x_off, out, y)))
+    return sum(vals) / max(len(vals), 1)
+
+
+def fit(model, train_loader, test_loader=None, epochs=100, lr=1e-3, per_epoch_schedule=True, checkpoint=None,
+        log=print):
+    """The reference training loop (main.py:50-153) on packed batches: AdamW(lr) + OneCycleLR(max_lr=lr,
+    steps_per_epoch, epochs), RelL2 loss, per-epoch test metric and best checkpoint.  With
+    per_epoch_schedule=True the schedule is stepped once per epoch, as main.py:106 does.
+    Returns (train losses per epoch, test metrics per epoch)."""
+    dev = next(model.parameters()).device
+    flat = flatten_parameters(model)
+    sched = OneCycle(lr, epochs, len(train_loader))
+    opt = FlatAdamW(flat, lr=lr, schedule=sched)
+    eng = model.engine()
+    eng.param_grads = False
+    loss_fn = RelL2Loss()
+    best, hist_train, hist_test = float("inf"), [], []
+    for epoch in range(epochs):
+        losses = []
+        for batch in train_loader:
+            x, x_off, theta, fns, fn_offs, y = _to(batch, dev)
+            out = model.forward_packed(x, x_off, theta, fns, fn_offs)
+            loss = loss_fn(x_off, out, y)
+            loss.backward()
+            opt.step(eng.grad_flat)
+            if not per_epoch_schedule:
+                sched.step()
+            losses.append(float(loss))
+        if per_epoch_schedule:
+            sched.step()
+        hist_train.append(sum(losses) / max(len(losses), 1))
+        log(f"Epoch {epoch}, Loss: {hist_train[-1]}")
+        if test_loader is not None:
+            res = evaluate(model, test_loader, loss_fn)
+            hist_test.append(res)
+            log(f"Epoch {epoch}, Test Metric: {res}")
+            if res < best and checkpoint:
+                best = res
+                save_checkpoint(model, checkpoint)
+    return hist_train, hist_test
