@@ -33,11 +33,11 @@ __global__ void __launch_bounds__(64 * kChainWaves) chain_fwd_kernel(ChainArgs a
   const int nl = a.nlin;
   const ChainLayer* L = a.layers + e * nl;
   float* save = a.save ? a.save + e * a.save_chain_stride : nullptr;
-  __shared__ __attribute__((aligned(16))) float4 wlds[2 * kChunkF4];
+  __shared__ __attribute__((aligned(16))) float4 wlds[2 * x6_buf_f4(D)];
   int cnt = 0;
   // the weight stream: layer 0 | hidden layers | last layer, one chunk always in flight
-  stage_image(wlds, L[0].Wp, chunk_f4(KT0, DT), kChainWaves, wave, lane);
-  auto next_f4 = [&](int l) { return (l == nl - 1) ? chunk_f4(DT, OTL) : chunk_f4(DT, DT); };
+  stage_image(wlds, L[0].Wp, x6_chunk_f4<D>(KT0, DT), kChainWaves, wave, lane);
+  auto next_f4 = [&](int l) { return (l == nl - 1) ? x6_chunk_f4<D>(DT, OTL) : x6_chunk_f4<D>(DT, DT); };
 
   float h[DT][4];
   {
@@ -45,7 +45,7 @@ __global__ void __launch_bounds__(64 * kChainWaves) chain_fwd_kernel(ChainArgs a
     load_rows<KT0>(x0, a.X, a.ldx, p, valid, a.in_dim, lane);
     f32x4 acc[DT];
     init_bias<DT>(acc, L[0].bias, lane);
-    mm_tiles_pipe<KT0, DT>(L[0].Wp, L[1].Wp, next_f4(1), wlds, cnt, x0, acc, kChainWaves, wave, lane);
+    mm_tiles_pipe_x6<D, KT0, DT>(L[0].Wp, L[1].Wp, next_f4(1), wlds, cnt, x0, acc, kChainWaves, wave, lane);
     acc_to_regs<DT>(acc, h);
   }
   if (save) store_rows<DT>(h, save, D, p, valid, D, lane);
@@ -57,7 +57,7 @@ __global__ void __launch_bounds__(64 * kChainWaves) chain_fwd_kernel(ChainArgs a
   for (int l = 1; l < nl - 1; ++l) {
     f32x4 acc[DT];
     init_bias<DT>(acc, L[l].bias, lane);
-    mm_tiles_pipe<DT, DT>(L[l].Wp, L[l + 1].Wp, next_f4(l + 1), wlds, cnt, h, acc, kChainWaves, wave, lane);
+    mm_tiles_pipe_x6<D, DT, DT>(L[l].Wp, L[l + 1].Wp, next_f4(l + 1), wlds, cnt, h, acc, kChainWaves, wave, lane);
     acc_to_regs<DT>(acc, h);
     if (save) store_rows<DT>(h, save + l * a.save_layer_stride, D, p, valid, D, lane);
 #pragma unroll
@@ -70,7 +70,7 @@ __global__ void __launch_bounds__(64 * kChainWaves) chain_fwd_kernel(ChainArgs a
   {
     f32x4 acc[OTL];
     init_bias<OTL>(acc, L[nl - 1].bias, lane);
-    mm_tiles_pipe<DT, OTL>(L[nl - 1].Wp, nullptr, 0, wlds, cnt, h, acc, kChainWaves, wave, lane);
+    mm_tiles_pipe_x6<D, DT, OTL>(L[nl - 1].Wp, nullptr, 0, wlds, cnt, h, acc, kChainWaves, wave, lane);
     acc_to_regs<OTL>(acc, y);
   }
   if (save) store_rows<OTL>(y, save + (nl - 1) * a.save_layer_stride, D, p, valid, 16 * OTL, lane);

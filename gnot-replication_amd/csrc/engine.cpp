@@ -364,14 +364,24 @@ static void plan_images(gnot_plan* p) {
     p->packed4 += (size_t)OT * KT * 64;
     return im;
   };
+  // bf16x6 image (chain kernels): OT x ceil(KT/2) blocks of 3 pieces x 64 lanes x 16 B
+  auto new_img_x6 = [&](int OT, int KT) {
+    Img im;
+    im.off4 = p->packed4;
+    im.OT = OT;
+    im.KT = KT;
+    p->packed4 += (size_t)OT * ((KT + 1) / 2) * 3 * 64;
+    return im;
+  };
   auto new_bias = [&](int n) {
     const size_t o = p->pbias;
     p->pbias += (size_t)((n + 63) / 64) * 64;
     return o;
   };
   // job: linear li into image im at tile offsets (o0, t0); transposed flag; bias destination
-  auto job = [&](int li, const Img& im, int o0, int t0, int OTp, int KTp, int tr, long bias_off) {
+  auto job = [&](int li, const Img& im, int o0, int t0, int OTp, int KTp, int tr, long bias_off, int x6 = 0) {
     PackJob J{};
+    J.x6 = x6;
     J.out = p->lin_o[li];
     J.in = p->lin_i[li];
     J.transposed = tr;
@@ -388,10 +398,10 @@ static void plan_images(gnot_plan* p) {
       const int li = first + j;
       const int KTp = (j == 0) ? KT0 : DT;
       const int OTp = (j == NL - 1) ? OTL : DT;
-      Img f = new_img(OTp, KTp);
+      Img f = new_img_x6(OTp, KTp);
       const size_t bo = new_bias(16 * OTp);
-      job(li, f, 0, 0, OTp, KTp, 0, (long)bo);
-      Img t = new_img(KTp, OTp);
+      job(li, f, 0, 0, OTp, KTp, 0, (long)bo, 1);
+      Img t = new_img(KTp, OTp);          // backward-data image: exact fp32 MFMA (chain_bwd)
       job(li, t, 0, 0, KTp, OTp, 1, -1);
       p->fwd_img[li] = f;
       p->T_img[li] = t;
@@ -453,7 +463,7 @@ static void plan_images(gnot_plan* p) {
   int acc = 0;
   for (auto& J : p->pack_jobs) {
     p->pack_prefix.push_back(acc);
-    acc += J.OTp * J.KTp;
+    acc += pack_tiles(J);
   }
   p->pack_tiles = acc;
 }

@@ -246,6 +246,127 @@ GNOT_DEV void mm_tiles_pipe(const float4* __restrict__ Wg, const float4* __restr
   }
 }
 
+// ---- fp32 GEMM on bf16 MFMAs, split three ways ("bf16x6") --------------------------------------
+// Every fp32 operand is written EXACTLY as the sum of three bf16 pieces by truncation
+// (v = v0 + v1 + v2: each piece keeps the next 8 significant bits of the 24-bit mantissa), and a
+// product as the six terms of order <= 2:  a.b ~ a0b0 + (a0b1 + a1b0) + (a0b2 + a1b1 + a2b0).  Each
+// term is an exact product of 8-bit mantissas; the dropped terms (a1b2, a2b1, a2b2) are < 2^-23
+// relative, i.e. fp32 rounding level, and the order-0 term accumulates separately from the small
+// ones.  Six v_mfma_f32_16x16x32_bf16 (16 cycles each) replace eight v_mfma_f32_16x16x4_f32 (32
+// cycles each) per 16x16x32 block: 2.7x fewer matrix-pipe cycles at fp32-level accuracy.
+//
+// Point form carries over unchanged: for k-block t (features 32t..32t+31) lane (p, g) feeds MFMA
+// k-slots 8g+j with its own registers: j < 4 -> feature 32t+4g+j (tile 2t), j >= 4 -> feature
+// 32t+16+4g+(j-4) (tile 2t+1).  Weight images (pack.hip, x6 jobs) use the same k order:
+// image[((o*KB + t)*3 + q)*64 + lane] = 8 bf16 of piece q of rows 16o+(lane&15), k-slots 8(lane>>4)+j.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// LDS buffer of the bf16x6 weight stream: at least one output tile's full-K image (ceil(DT/2)*3 KiB);
+// 24 KiB per buffer (measured at d = 128: 12 KiB buffers, 6 instead of 3 workgroups per CU, are slower)
+constexpr int x6_buf_kb(int) { return 24; }
+constexpr int x6_buf_f4(int D) { return x6_buf_kb(D) * WAVE; }   // 16-byte units per buffer
+
+template <int D>
+constexpr int x6_och(int KT, int OT) {                // output tiles per chunk (KB*3 KiB per tile)
+  int c = OT;
+  while (c > 1 && (c * ((KT + 1) / 2) * 3 > x6_buf_kb(D) || OT % c != 0)) --c;
+  return c;
+}
+template <int D>
+constexpr int x6_chunk_f4(int KT, int OT) { return x6_och<D>(KT, OT) * ((KT + 1) / 2) * 3 * WAVE; }
+
+GNOT_DEV unsigned f2u(float x) { return __builtin_bit_cast(unsigned, x); }
+GNOT_DEV float u2f(unsigned x) { return __builtin_bit_cast(float, x); }
+
+// B pieces of the point-form activations in[KT][4]: bp[q][t] = 8 bf16 (4 dwords) of piece q, block t
+template <int KT>
+GNOT_DEV void split_x6(const float (&in)[KT][4], u32x4 (&bp)[3][(KT + 1) / 2]) {
+#pragma unroll
+  for (int t = 0; t < (KT + 1) / 2; ++t) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[j] = in[2 * t][j];
+      v[4 + j] = (2 * t + 1 < KT) ? in[2 * t + 1][j] : 0.f;
+    }
+    unsigned w0[8], w1[8], w2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const unsigned b = f2u(v[j]);
+      const float r1 = v[j] - u2f(b & 0xFFFF0000u);
+      const unsigned b1 = f2u(r1);
+      const float r2 = r1 - u2f(b1 & 0xFFFF0000u);
+      w0[j] = b;
+      w1[j] = b1;
+      w2[j] = f2u(r2);
+    }
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      bp[0][t][d] = (w0[2 * d + 1] & 0xFFFF0000u) | (w0[2 * d] >> 16);
+      bp[1][t][d] = (w1[2 * d + 1] & 0xFFFF0000u) | (w1[2 * d] >> 16);
+      bp[2][t][d] = (w2[2 * d + 1] & 0xFFFF0000u) | (w2[2 * d] >> 16);
+    }
+  }
+}
+
+GNOT_DEV f32x4 mfma_bf16(const u32x4& a, const u32x4& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                 0, 0, 0);
+}
+
+// Same contract as mm_tiles_pipe (acc pre-initialised, chunks double-buffered in `lds` of
+// 2*kChunkX6F4 units, next image staged across the layer boundary, hook on the last chunk), for
+// x6 weight images.  acc gets the order-0 term; the order-1/2 terms accumulate in a second set of
+// accumulators that is added at the end.
+template <int D, int KT, int OT, typename Hook = NoHook>
+GNOT_DEV void mm_tiles_pipe_x6(const float4* __restrict__ Wg, const float4* __restrict__ next_W, int next_f4,
+                               float4* lds, int& cnt, const float (&in)[KT][4], f32x4 (&acc)[OT], int nwaves,
+                               int wave, int lane, Hook hook = Hook()) {
+  constexpr int kChunkX6F4 = x6_buf_f4(D);
+  constexpr int KB = (KT + 1) / 2;
+  constexpr int OCH = x6_och<D>(KT, OT);
+  constexpr int NC = OT / OCH;
+  constexpr int CH4 = OCH * KB * 3 * WAVE;
+  u32x4 bp[3][KB];
+  split_x6<KT>(in, bp);
+  f32x4 lo[OT];
+#pragma unroll
+  for (int o = 0; o < OT; ++o) lo[o] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    __syncthreads();
+    float4* nb = lds + ((cnt + 1) & 1) * kChunkX6F4;
+    if (c + 1 < NC) stage_image(nb, Wg + (c + 1) * CH4, CH4, nwaves, wave, lane);
+    else if (next_W) stage_image(nb, next_W, next_f4, nwaves, wave, lane);
+    if (c == 0) hook();
+    const u32x4* cb = reinterpret_cast<const u32x4*>(lds + (cnt & 1) * kChunkX6F4);
+#pragma unroll
+    for (int t = 0; t < KB; ++t) {
+      u32x4 a[OCH][3];
+#pragma unroll
+      for (int o = 0; o < OCH; ++o)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) a[o][q] = cb[((o * KB + t) * 3 + q) * WAVE + lane];
+#pragma unroll
+      for (int o = 0; o < OCH; ++o) acc[c * OCH + o] = mfma_bf16(a[o][0], bp[0][t], acc[c * OCH + o]);
+#pragma unroll
+      for (int o = 0; o < OCH; ++o) {
+        f32x4 l = lo[c * OCH + o];
+        l = mfma_bf16(a[o][0], bp[1][t], l);
+        l = mfma_bf16(a[o][1], bp[0][t], l);
+        l = mfma_bf16(a[o][0], bp[2][t], l);
+        l = mfma_bf16(a[o][1], bp[1][t], l);
+        l = mfma_bf16(a[o][2], bp[0][t], l);
+        lo[c * OCH + o] = l;
+      }
+    }
+    ++cnt;
+  }
+#pragma unroll
+  for (int o = 0; o < OT; ++o) acc[o] += lo[o];
+}
+
 template <int OT>
 GNOT_DEV void init_bias(f32x4 (&acc)[OT], const float* __restrict__ bias, int lane) {
   const int g = lane >> 4;

@@ -50,7 +50,7 @@ int main(int argc, char** argv) {
   const int D = argc > 2 ? std::atoi(argv[2]) : 128;
   const int E = 4, NL = 5, DT = D / 16;
   // packed weight images: NL layers x E chains, fwd and transposed (values arbitrary, finite)
-  const size_t img4 = (size_t)DT * DT * 64;     // float4 per DxD image
+  const size_t img4 = (size_t)DT * ((DT + 1) / 2) * 3 * 64;   // float4 per DxD image (bf16x6 >= fp32)
   float4* W = reinterpret_cast<float4*>(dalloc(img4 * 4 * NL * E * 2, 0.05f));
   float* bias = dalloc((size_t)NL * E * D, 0.01f);
   std::vector<ChainLayer> layers;

@@ -27,6 +27,42 @@ __global__ void __launch_bounds__(64) pack_kernel(const PackJob* __restrict__ jo
   const int t = tile_id - prefix[lo];
   const int lane = threadIdx.x;
   const int r16 = lane & 15, g = lane >> 4;
+  if (J.x6) {
+    // bf16x6 image block (o, kb): lane holds row 16o + r16 at k-slots 8g + j of k-block kb
+    const int KB = (J.KTp + 1) / 2;
+    const int o = t / KB, kb = t % KB;
+    unsigned w[3][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int f = 32 * kb + (j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4));   // contraction index
+      const int row = 16 * o + r16;
+      float v = 0.f;
+      if (!J.transposed) v = (row < J.out && f < J.in) ? J.W[(long)row * J.in + f] : 0.f;
+      else v = (f < J.out && row < J.in) ? J.W[(long)f * J.in + row] : 0.f;
+      const unsigned b = __builtin_bit_cast(unsigned, v);
+      const float r1 = v - __builtin_bit_cast(float, b & 0xFFFF0000u);
+      const unsigned b1 = __builtin_bit_cast(unsigned, r1);
+      const float r2 = r1 - __builtin_bit_cast(float, b1 & 0xFFFF0000u);
+      w[0][j] = b;
+      w[1][j] = b1;
+      w[2][j] = __builtin_bit_cast(unsigned, r2);
+    }
+    uint4* dst = reinterpret_cast<uint4*>(J.dst);
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      uint4 u;
+      u.x = (w[q][1] & 0xFFFF0000u) | (w[q][0] >> 16);
+      u.y = (w[q][3] & 0xFFFF0000u) | (w[q][2] >> 16);
+      u.z = (w[q][5] & 0xFFFF0000u) | (w[q][4] >> 16);
+      u.w = (w[q][7] & 0xFFFF0000u) | (w[q][6] >> 16);
+      dst[((long)(J.o0 + o) * ((J.ktot + 1) / 2) + J.t0 / 2 + kb) * 3 * WAVE + q * WAVE + lane] = u;
+    }
+    if (J.bias_dst && t == 0) {
+      const int nb = 16 * J.OTp;
+      for (int i = lane; i < nb; i += WAVE) J.bias_dst[i] = (i < J.out && J.b) ? J.b[i] : 0.f;
+    }
+    return;
+  }
   float v[4];
   int o, T;
   if (!J.transposed) {
