@@ -49,6 +49,13 @@ GNOT_DEV float group_sum(float v) {
   return v;
 }
 
+// compiler-only fence: keeps the k-loop's state loads from being hoisted all at once (at dh >= 32 that
+// pushes a lane past 128 VGPRs); one in-flight block of kRowBlock rows is enough latency cover
+constexpr int kRowBlock = 16;
+GNOT_DEV void row_block_fence(int k) {
+  if ((k + 1) % kRowBlock == 0) asm volatile("" ::: "memory");
+}
+
 template <int N>
 GNOT_DEV void load_vec(float (&dst)[N], const float* __restrict__ src) {
 #pragma unroll
@@ -82,6 +89,38 @@ GNOT_DEV bool decode_task(const int4& ch, int H, Task& t) {
   return true;
 }
 
+// group-transposed row sums: lane q of a G-lane group holds v[k] = sum over ITS feature slice of
+// row k (k = 0 .. DH-1); returns in v[0 .. C) the group total of rows q*C .. q*C+C-1 (a butterfly
+// reduce-scatter: log2(G) shfl_xor stages, each halving the rows a lane carries).  This replaces
+// re-reading whole state rows per lane: a group reads each (S, z) element exactly once.
+template <int G, int C>
+GNOT_DEV void group_reduce_scatter(float (&v)[G * C], int q) {
+#pragma unroll
+  for (int m = G / 2; m >= 1; m >>= 1) {
+    const bool up = (q & m) != 0;
+#pragma unroll
+    for (int i = 0; i < m * C; ++i) {
+      const float lo = v[i], hi = v[i + m * C];
+      const float send = up ? lo : hi;
+      const float keep = up ? hi : lo;
+      v[i] = keep + __shfl_xor(send, m, 64);
+    }
+  }
+}
+
+// den = q . z for the group's (point, head): each lane dots its own slice, then a group sum
+// (qs = the lane's own q slice, loaded separately: indexing the full q[DH] registers at the
+// lane-dependent offset c0 would compile to select chains)
+template <int G, int C>
+GNOT_DEV float group_den(const float (&qs)[C], const float* __restrict__ z, int c0) {
+  float zs[C];
+  load_vec<C>(zs, z + c0);
+  float d = 0.f;
+#pragma unroll
+  for (int c = 0; c < C; ++c) d = fmaf(qs[c], zs[c], d);
+  return group_sum<G>(d);
+}
+
 // ---------------------------------------------------------------- apply (forward)
 template <int DH>
 __global__ void __launch_bounds__(256) attn_apply_fwd_kernel(AttnApplyArgs a) {
@@ -94,24 +133,25 @@ __global__ void __launch_bounds__(256) attn_apply_fwd_kernel(AttnApplyArgs a) {
   const long off_b = a.off[b];
   const long Nb = a.off[b + 1] - off_b;
   const int c0 = t.q * C;
-  float qf[DH];
+  float qf[DH], qs[C];
   load_vec<DH>(qf, a.q + t.n * a.ldq + t.h * DH);
+  load_vec<C>(qs, a.q + t.n * a.ldq + t.h * DH + c0);
   float os[C];
 #pragma unroll
   for (int c = 0; c < C; ++c) os[c] = 0.f;
   for (int s = 0; s < a.nsrc; ++s) {
     const float* S = a.state[s] + (long)b * a.H * ph + t.h * ph;
-    const float* z = S + DH * DH;
-    float den = 0.f, u[C];
+    const float den = group_den<G, C>(qs, S + DH * DH, c0);
+    float u[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) u[c] = 0.f;
 #pragma unroll
     for (int k = 0; k < DH; ++k) {
-      den = fmaf(qf[k], z[k], den);
       float srow[C];
       load_vec<C>(srow, S + k * DH + c0);
 #pragma unroll
       for (int c = 0; c < C; ++c) u[c] = fmaf(qf[k], srow[c], u[c]);
+      row_block_fence(k);
     }
     const float inv = 1.0f / den;
 #pragma unroll
@@ -120,13 +160,15 @@ __global__ void __launch_bounds__(256) attn_apply_fwd_kernel(AttnApplyArgs a) {
   const float inv_nsrc = 1.0f / (float)a.nsrc;
   float r[C];
 #pragma unroll
-  for (int c = 0; c < C; ++c) r[c] = fmaf(os[c], inv_nsrc, qf[c0 + c]);
+  for (int c = 0; c < C; ++c) r[c] = fmaf(os[c], inv_nsrc, qs[c]);
   store_vec<C>(a.res + off_b * (long)a.H * DH + ((long)t.h * Nb + (t.n - off_b)) * DH + c0, r);
 }
 
 // ---------------------------------------------------------------- apply (backward)
 // dO = dres/nsrc; per source: o = u/den, du = dO/den, dden = -(dO.u)/den^2, dq += du S^T + dden z;
-// dq starts at dres (the q residual); finally the feature-softmax backward of q.
+// dq starts at dres (the q residual); finally the feature-softmax backward of q.  One pass over the
+// lane's column slice of S gives both u (columns) and the lane's share of S dO (rows, finished by
+// the group reduce-scatter).
 template <int DH>
 __global__ void __launch_bounds__(256) attn_apply_bwd_kernel(AttnApplyArgs a) {
   constexpr int G = HeadSplit<DH>::G, C = HeadSplit<DH>::C;
@@ -139,62 +181,67 @@ __global__ void __launch_bounds__(256) attn_apply_bwd_kernel(AttnApplyArgs a) {
   const long Nb = a.off[b + 1] - off_b;
   const int c0 = t.q * C;
   const float inv_nsrc = 1.0f / (float)a.nsrc;
-  float qf[DH], dOf[DH];
+  float qf[DH], qs[C], dO[C];
   load_vec<DH>(qf, a.q + t.n * a.ldq + t.h * DH);
-  load_vec<DH>(dOf, a.dres + off_b * (long)a.H * DH + ((long)t.h * Nb + (t.n - off_b)) * DH);
+  load_vec<C>(qs, a.q + t.n * a.ldq + t.h * DH + c0);
+  load_vec<C>(dO, a.dres + off_b * (long)a.H * DH + ((long)t.h * Nb + (t.n - off_b)) * DH + c0);
   float dq[C];
 #pragma unroll
-  for (int c = 0; c < C; ++c) dq[c] = dOf[c0 + c];
-#pragma unroll
-  for (int j = 0; j < DH; ++j) dOf[j] *= inv_nsrc;
+  for (int c = 0; c < C; ++c) {
+    dq[c] = dO[c];
+    dO[c] *= inv_nsrc;
+  }
   for (int s = 0; s < a.nsrc; ++s) {
     const float* S = a.state[s] + (long)b * a.H * ph + t.h * ph;
     const float* z = S + DH * DH;
-    float den = 0.f, u[C];
+    const float den = group_den<G, C>(qs, z, c0);
+    float u[C], part[DH];
 #pragma unroll
     for (int c = 0; c < C; ++c) u[c] = 0.f;
 #pragma unroll
     for (int k = 0; k < DH; ++k) {
-      den = fmaf(qf[k], z[k], den);
       float srow[C];
       load_vec<C>(srow, S + k * DH + c0);
+      float pk = 0.f;
 #pragma unroll
-      for (int c = 0; c < C; ++c) u[c] = fmaf(qf[k], srow[c], u[c]);
+      for (int c = 0; c < C; ++c) {
+        u[c] = fmaf(qf[k], srow[c], u[c]);
+        pk = fmaf(dO[c], srow[c], pk);
+      }
+      part[k] = pk;
+      row_block_fence(k);
     }
     float dot = 0.f;
 #pragma unroll
-    for (int c = 0; c < C; ++c) dot = fmaf(dOf[c0 + c], u[c], dot);
+    for (int c = 0; c < C; ++c) dot = fmaf(dO[c], u[c], dot);
     dot = group_sum<G>(dot);
     const float inv = 1.0f / den;
     const float dden = -dot * inv * inv;
     float du[C];
 #pragma unroll
-    for (int c = 0; c < C; ++c) du[c] = dOf[c0 + c] * inv;
+    for (int c = 0; c < C; ++c) du[c] = dO[c] * inv;
     store_vec<C>(a.du[s] + t.n * a.lddu + t.h * DH + c0, du);
     if (t.q == 0) a.dden[s][t.n * a.H + t.h] = dden;
-    // dq[k] += sum_j du_j S[k][j] + dden z[k] for this lane's rows k = c0 .. c0+C-1 (du = dO * inv)
+    // dq[k] += (sum_j dO_j S[k][j]) / den + dden z[k] for this lane's rows k = c0 .. c0+C-1
+    group_reduce_scatter<G, C>(part, t.q);
+    float zs[C];
+    load_vec<C>(zs, z + c0);
 #pragma unroll
-    for (int c = 0; c < C; ++c) {
-      float srow[DH];
-      load_vec<DH>(srow, S + (c0 + c) * DH);
-      float acc = 0.f;
-#pragma unroll
-      for (int j = 0; j < DH; ++j) acc = fmaf(dOf[j], srow[j], acc);
-      dq[c] = fmaf(acc, inv, fmaf(dden, z[c0 + c], dq[c]));
-    }
+    for (int c = 0; c < C; ++c) dq[c] = fmaf(part[c], inv, fmaf(dden, zs[c], dq[c]));
   }
   float qdq = 0.f;
 #pragma unroll
-  for (int c = 0; c < C; ++c) qdq = fmaf(qf[c0 + c], dq[c], qdq);
+  for (int c = 0; c < C; ++c) qdq = fmaf(qs[c], dq[c], qdq);
   qdq = group_sum<G>(qdq);
   float dpre[C];
 #pragma unroll
-  for (int c = 0; c < C; ++c) dpre[c] = qf[c0 + c] * (dq[c] - qdq);
+  for (int c = 0; c < C; ++c) dpre[c] = qs[c] * (dq[c] - qdq);
   store_vec<C>(a.dq_pre + t.n * a.lddq + t.h * DH + c0, dpre);
 }
 
 // ---------------------------------------------------------------- K/V backward
-// dk = dz + v dS^T, dv = k dS (per head), then the feature-softmax backward of k.
+// dk = dz + v dS^T, dv = k dS (per head), then the feature-softmax backward of k.  One pass over the
+// lane's column slice of dS: dv (columns) directly, dk (rows) through the group reduce-scatter.
 template <int DH>
 GNOT_DEV void attn_kv_bwd_body(const AttnKVBwdArgs& a, const int4& ch) {
   constexpr int G = HeadSplit<DH>::G, C = HeadSplit<DH>::C;
@@ -205,33 +252,37 @@ GNOT_DEV void attn_kv_bwd_body(const AttnKVBwdArgs& a, const int4& ch) {
   const int c0 = t.q * C;
   const float* dS = a.dstate + (long)b * a.H * ph + t.h * ph;
   const float* dz = dS + DH * DH;
-  float kf[DH], vf[DH];
+  float kf[DH], ks[C], vs[C];
   load_vec<DH>(kf, a.k + t.n * a.ldkv + t.h * DH);
-  load_vec<DH>(vf, a.v + t.n * a.ldkv + t.h * DH);
-  float dk[C], dv[C];
+  load_vec<C>(ks, a.k + t.n * a.ldkv + t.h * DH + c0);
+  load_vec<C>(vs, a.v + t.n * a.ldkv + t.h * DH + c0);
+  float dv[C], part[DH];
 #pragma unroll
-  for (int c = 0; c < C; ++c) {
-    float srow[DH];
-    load_vec<DH>(srow, dS + (c0 + c) * DH);
-    float acc = dz[c0 + c];
-#pragma unroll
-    for (int j = 0; j < DH; ++j) acc = fmaf(vf[j], srow[j], acc);
-    dk[c] = acc;
-    dv[c] = 0.f;
-  }
+  for (int c = 0; c < C; ++c) dv[c] = 0.f;
 #pragma unroll
   for (int i = 0; i < DH; ++i) {
     float srow[C];
     load_vec<C>(srow, dS + i * DH + c0);
+    float pk = 0.f;
 #pragma unroll
-    for (int c = 0; c < C; ++c) dv[c] = fmaf(kf[i], srow[c], dv[c]);
+    for (int c = 0; c < C; ++c) {
+      dv[c] = fmaf(kf[i], srow[c], dv[c]);
+      pk = fmaf(vs[c], srow[c], pk);
+    }
+    part[i] = pk;
+    row_block_fence(i);
   }
+  group_reduce_scatter<G, C>(part, t.q);
+  float dzs[C], dk[C];
+  load_vec<C>(dzs, dz + c0);
+#pragma unroll
+  for (int c = 0; c < C; ++c) dk[c] = dzs[c] + part[c];
   float kdk = 0.f;
 #pragma unroll
-  for (int c = 0; c < C; ++c) kdk = fmaf(kf[c0 + c], dk[c], kdk);
+  for (int c = 0; c < C; ++c) kdk = fmaf(ks[c], dk[c], kdk);
   kdk = group_sum<G>(kdk);
 #pragma unroll
-  for (int c = 0; c < C; ++c) dk[c] = kf[c0 + c] * (dk[c] - kdk);
+  for (int c = 0; c < C; ++c) dk[c] = ks[c] * (dk[c] - kdk);
   store_vec<C>(a.dk + t.n * a.lddkv + t.h * DH + c0, dk);
   store_vec<C>(a.dv + t.n * a.lddkv + t.h * DH + c0, dv);
 }

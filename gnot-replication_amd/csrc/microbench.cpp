@@ -125,6 +125,45 @@ int main(int argc, char** argv) {
     float* slab = dalloc((size_t)slab_off, 0.f);
     t = time_us([&] { CK(launch_wgrad(djobs, dpre, njobs, wg, dpre + njobs, red, slab, nullptr)); }, 20);
     std::printf("wgrad MoE  %d jobs P=%d D=%d (%d WGs): %8.2f us  %6.1f TFLOP/s\n", njobs, P, D, wg, t, fl / t / 1e6);
+
+    // attention apply pass (H = 8 heads of D/8), alone and under a concurrent MoE wgrad stream
+    const int H = 8, dh = D / H;
+    std::vector<int4> ch;
+    for (int s0 = 0; s0 < P; s0 += 64) ch.push_back(make_int4(0, s0, std::min(64, P - s0), 0));
+    int4* dch = nullptr;
+    CK(hipMalloc(&dch, ch.size() * sizeof(int4)));
+    CK(hipMemcpy(dch, ch.data(), ch.size() * sizeof(int4), hipMemcpyHostToDevice));
+    long* doff = nullptr;
+    const long hoff[2] = {0, P};
+    CK(hipMalloc(&doff, sizeof(hoff)));
+    CK(hipMemcpy(doff, hoff, sizeof(hoff), hipMemcpyHostToDevice));
+    float* st = dalloc((size_t)2 * H * (dh * dh + dh), 0.1f);
+    float* q = dalloc((size_t)P * 3 * D, 0.05f);
+    float* dres = dalloc((size_t)P * D, 0.3f);
+    float* du = dalloc((size_t)2 * P * D, 0.f);
+    float* dden = dalloc((size_t)2 * P * H, 0.f);
+    float* dq = dalloc((size_t)P * 3 * D, 0.f);
+    hipStream_t s2;
+    CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+    for (int nsrc : {1, 2}) {
+      AttnApplyArgs ap{};
+      ap.q = q; ap.ldq = nsrc == 1 ? 3 * D : D; ap.nsrc = nsrc; ap.chunks = dch; ap.nchunks = (int)ch.size();
+      ap.off = doff; ap.H = H; ap.dh = dh; ap.res = Y; ap.dres = dres; ap.dq_pre = dq; ap.lddq = ap.ldq; ap.lddu = D;
+      for (int i = 0; i < nsrc; ++i) {
+        ap.state[i] = st + (size_t)i * H * (dh * dh + dh);
+        ap.du[i] = du + (size_t)i * P * D;
+        ap.dden[i] = dden + (size_t)i * P * H;
+      }
+      t = time_us([&] { CK(launch_attn_apply_fwd(ap, nullptr)); });
+      std::printf("apply_fwd  nsrc=%d P=%d H=%d dh=%d: %8.2f us\n", nsrc, P, H, dh, t);
+      t = time_us([&] { CK(launch_attn_apply_bwd(ap, nullptr)); });
+      std::printf("apply_bwd  nsrc=%d P=%d H=%d dh=%d: %8.2f us\n", nsrc, P, H, dh, t);
+      // contention: wgrad launches queued on s2 while apply_bwd is timed on the null stream
+      for (int i = 0; i < 30; ++i) CK(launch_wgrad(djobs, dpre, njobs, wg, dpre + njobs, red, slab, s2));
+      t = time_us([&] { CK(launch_attn_apply_bwd(ap, nullptr)); }, 20);
+      std::printf("apply_bwd  nsrc=%d under concurrent wgrad: %8.2f us\n", nsrc, t);
+      CK(hipStreamSynchronize(s2));
+    }
   }
   CK(hipDeviceSynchronize());
   return 0;
