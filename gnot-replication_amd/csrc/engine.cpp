@@ -61,6 +61,7 @@ struct WgradGroup {
   std::vector<int> wg_prefix, red_prefix;
   int total_wgs = 0, total_red = 0;
   size_t slab_floats = 0;
+  bool x6 = false;                   // plain weight-gradient jobs: the bf16x6 MFMA kernel
   WgradJob* d_jobs = nullptr;        // device copies (workspace tables)
   int* d_wg_prefix = nullptr;
   int* d_red_prefix = nullptr;
@@ -496,6 +497,11 @@ static void finish_group(gnot_plan* p, WgradGroup& G) {
   }
   G.total_wgs = wg;
   G.total_red = red;
+  // env GNOT_WGRAD_FP32: weight gradients on the fp32 MFMA kernel (diagnostics)
+  static const bool fp32_only = std::getenv("GNOT_WGRAD_FP32") != nullptr;
+  G.x6 = !fp32_only;
+  for (const auto& J : G.jobs)
+    if (J.w != nullptr || J.state_dh > 0 || J.diag_only) G.x6 = false;
   size_t& slab = (!G.jobs.empty() && G.jobs[0].state_dh > 0) ? p->slab_state_floats : p->slab_wgrad_floats;
   slab = std::max(slab, G.slab_floats);
 }
@@ -1324,7 +1330,7 @@ int run_wgrad_side(Ctx& c, const WgradGroup& G, std::initializer_list<const floa
     float* slab = c.s == p->side2 ? p->P_("slab_wgrad2") : p->P_("slab_wgrad");
     ProfScope ps(c, "wgrad", group_flops(G));
     GNOT_CK(launch_wgrad(G.d_jobs, G.d_wg_prefix, (int)G.jobs.size(), G.total_wgs, G.d_red_prefix,
-                         G.total_red, slab, c.s));
+                         G.total_red, slab, c.s, G.x6));
     return GNOT_OK;
   }
   hipEvent_t fork = next_event(p);
@@ -1333,7 +1339,7 @@ int run_wgrad_side(Ctx& c, const WgradGroup& G, std::initializer_list<const floa
   {
     ProfScope ps(c, "wgrad", group_flops(G), p->side);
     GNOT_CK(launch_wgrad(G.d_jobs, G.d_wg_prefix, (int)G.jobs.size(), G.total_wgs, G.d_red_prefix,
-                         G.total_red, p->P_("slab_wgrad"), p->side));
+                         G.total_red, p->P_("slab_wgrad"), p->side, G.x6));
   }
   hipEvent_t done = next_event(p);
   GNOT_CK(hipEventRecord(done, p->side));

@@ -279,6 +279,28 @@ constexpr int x6_chunk_f4(int KT, int OT) { return x6_och<D>(KT, OT) * ((KT + 1)
 GNOT_DEV unsigned f2u(float x) { return __builtin_bit_cast(unsigned, x); }
 GNOT_DEV float u2f(unsigned x) { return __builtin_bit_cast(float, x); }
 
+// exact 3-piece truncation split of 8 floats: p[q] = 8 bf16 (4 dwords, element j in the low half
+// of dword j/2 for even j) of piece q; v == piece0 + piece1 + piece2 exactly
+GNOT_DEV void split8_x6(const float (&v)[8], u32x4 (&p)[3]) {
+  unsigned w0[8], w1[8], w2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const unsigned b = f2u(v[j]);
+    const float r1 = v[j] - u2f(b & 0xFFFF0000u);
+    const unsigned b1 = f2u(r1);
+    const float r2 = r1 - u2f(b1 & 0xFFFF0000u);
+    w0[j] = b;
+    w1[j] = b1;
+    w2[j] = f2u(r2);
+  }
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    p[0][d] = (w0[2 * d + 1] & 0xFFFF0000u) | (w0[2 * d] >> 16);
+    p[1][d] = (w1[2 * d + 1] & 0xFFFF0000u) | (w1[2 * d] >> 16);
+    p[2][d] = (w2[2 * d + 1] & 0xFFFF0000u) | (w2[2 * d] >> 16);
+  }
+}
+
 // B pieces of the point-form activations in[KT][4]: bp[q][t] = 8 bf16 (4 dwords) of piece q, block t
 template <int KT>
 GNOT_DEV void split_x6(const float (&in)[KT][4], u32x4 (&bp)[3][(KT + 1) / 2]) {
@@ -290,23 +312,10 @@ GNOT_DEV void split_x6(const float (&in)[KT][4], u32x4 (&bp)[3][(KT + 1) / 2]) {
       v[j] = in[2 * t][j];
       v[4 + j] = (2 * t + 1 < KT) ? in[2 * t + 1][j] : 0.f;
     }
-    unsigned w0[8], w1[8], w2[8];
+    u32x4 p[3];
+    split8_x6(v, p);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const unsigned b = f2u(v[j]);
-      const float r1 = v[j] - u2f(b & 0xFFFF0000u);
-      const unsigned b1 = f2u(r1);
-      const float r2 = r1 - u2f(b1 & 0xFFFF0000u);
-      w0[j] = b;
-      w1[j] = b1;
-      w2[j] = f2u(r2);
-    }
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      bp[0][t][d] = (w0[2 * d + 1] & 0xFFFF0000u) | (w0[2 * d] >> 16);
-      bp[1][t][d] = (w1[2 * d + 1] & 0xFFFF0000u) | (w1[2 * d] >> 16);
-      bp[2][t][d] = (w2[2 * d + 1] & 0xFFFF0000u) | (w2[2 * d] >> 16);
-    }
+    for (int q = 0; q < 3; ++q) bp[q][t] = p[q];
   }
 }
 

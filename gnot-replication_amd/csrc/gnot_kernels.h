@@ -102,8 +102,9 @@ struct WgradJob {
 };
 // one workgroup per (job, tile, split); wg_prefix / red_prefix: per-job prefix sums of workgroups and
 // of reduce elements (ntile * 128 * 129)
+// x6: plain weight-gradient jobs only (no w, state_dh, diag_only) on the bf16x6 MFMA kernel
 hipError_t launch_wgrad(const WgradJob* jobs_dev, const int* wg_prefix_dev, int njobs, int total_wgs,
-                        const int* red_prefix_dev, int total_red, float* slab, hipStream_t s);
+                        const int* red_prefix_dev, int total_red, float* slab, hipStream_t s, bool x6 = false);
 
 // ------------------------------------------------------------------ attention states (state.hip)
 // Jobs are WgradJobs with state_dh > 0: A = dz/lddz, B = x/ldx, optional w/ldw, out = dW as

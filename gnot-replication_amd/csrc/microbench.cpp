@@ -5,6 +5,7 @@
 
 #include <cstdio>
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <vector>
 
@@ -91,6 +92,14 @@ int main(int argc, char** argv) {
     t = time_us([&] { CK(launch_linear(l, D, nullptr)); });
     std::printf("linear     P=%d K=%d NO=%d: %8.2f us  %6.1f TFLOP/s\n", P, D, NO, t, 2.0 * P * D * NO / t / 1e6);
   }
+  {  // finite dZ for the weight-gradient runs (the chain_bwd above wrote arbitrary values)
+    float* fresh = dalloc((size_t)E * NL * P * D, 0.5f);
+    CK(hipMemcpy(dz, fresh, (size_t)E * NL * P * D * 4, hipMemcpyDeviceToDevice));
+    CK(hipFree(fresh));
+    fresh = dalloc((size_t)E * NL * P * D, 2.0f);
+    CK(hipMemcpy(save, fresh, (size_t)E * NL * P * D * 4, hipMemcpyDeviceToDevice));
+    CK(hipFree(fresh));
+  }
   // weight-gradient point-reduction GEMM of one MoE chain group: E*NL jobs of D x D over P points,
   // split-K exactly as the engine sizes it (<= 512 workgroups, >= 128 points per split)
   {
@@ -125,6 +134,30 @@ int main(int argc, char** argv) {
     float* slab = dalloc((size_t)slab_off, 0.f);
     t = time_us([&] { CK(launch_wgrad(djobs, dpre, njobs, wg, dpre + njobs, red, slab, nullptr)); }, 20);
     std::printf("wgrad MoE  %d jobs P=%d D=%d (%d WGs): %8.2f us  %6.1f TFLOP/s\n", njobs, P, D, wg, t, fl / t / 1e6);
+    const size_t ndw = (size_t)E * NL * (D * D + D);
+    std::vector<float> ref(ndw), got(ndw);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(ref.data(), dW, ndw * 4, hipMemcpyDeviceToHost));
+    t = time_us([&] { CK(launch_wgrad(djobs, dpre, njobs, wg, dpre + njobs, red, slab, nullptr, true)); }, 20);
+    CK(hipDeviceSynchronize());
+    CK(hipMemcpy(got.data(), dW, ndw * 4, hipMemcpyDeviceToHost));
+    double num = 0, den = 0;
+    for (size_t i = 0; i < ndw; ++i) { num += (got[i] - ref[i]) * (double)(got[i] - ref[i]); den += (double)ref[i] * ref[i]; }
+    std::printf("wgrad MoE  bf16x6:                     %8.2f us  %6.1f TFLOP/s  (rel-L2 vs fp32 %.2e)\n", t, fl / t / 1e6,
+                std::sqrt(num / (den + 1e-30)));
+    {
+      std::vector<WgradJob> ng(jobs);
+      for (auto& J : ng) J.x_gelu = 0;
+      WgradJob* dng = nullptr;
+      CK(hipMalloc(&dng, ng.size() * sizeof(WgradJob)));
+      CK(hipMemcpy(dng, ng.data(), ng.size() * sizeof(WgradJob), hipMemcpyHostToDevice));
+      t = time_us([&] { CK(launch_wgrad(dng, dpre, njobs, wg, dpre + njobs, red, slab, nullptr)); }, 20);
+      std::printf("wgrad MoE  no-GELU operand:            %8.2f us  %6.1f TFLOP/s\n", t, fl / t / 1e6);
+      for (auto& J : ng) { J.x_gelu = 1; J.lddz = 0; J.ldx = 0; }   // every point reads row 0: no HBM traffic
+      CK(hipMemcpy(dng, ng.data(), ng.size() * sizeof(WgradJob), hipMemcpyHostToDevice));
+      t = time_us([&] { CK(launch_wgrad(dng, dpre, njobs, wg, dpre + njobs, red, slab, nullptr)); }, 20);
+      std::printf("wgrad MoE  L2-resident rows (diag):    %8.2f us  %6.1f TFLOP/s\n", t, fl / t / 1e6);
+    }
 
     // attention apply pass (H = 8 heads of D/8), alone and under a concurrent MoE wgrad stream
     const int H = 8, dh = D / H;

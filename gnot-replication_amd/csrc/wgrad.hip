@@ -171,6 +171,140 @@ __global__ void __launch_bounds__(256) pgemm_kernel(const WgradJob* __restrict__
   }
 }
 
+// ---------------------------------------------------------------- bf16x6 variant (plain weight-gradient jobs)
+// Same tiling, split-K and slab as pgemm_kernel, on v_mfma_f32_32x32x16_bf16: every staged fp32 value
+// is split exactly into three bf16 pieces (split8_x6) and each 32x32x16 block product is the six
+// order <= 2 piece products, accumulated in fp32 (the dropped terms are ~2^-24 relative: fp32-level,
+// like the forward chains; one accumulator per block keeps two workgroups per CU within the register
+// file): 6 x 32 = 192 matrix-pipe cycles per 32x32x16 block
+// instead of 8 x 64 = 512 on v_mfma_f32_32x32x2_f32.
+// Staging: thread (f = t & 127, g = t >> 7) loads feature f of 16 consecutive points (dword loads,
+// each wave-instruction reading 256 contiguous bytes of one row), so 8 consecutive points of one
+// feature are register-local and go to LDS as one 16-byte piece vector per piece: the LDS image is
+// [operand][piece][feature][point] with an 80-byte feature row (32 points + pad), which makes the
+// MFMA fragment read (lane = feature, 8 consecutive points) a conflict-free ds_read_b128.
+constexpr int kX6Stage = 32;                 // points per stage = two 16-point MFMA k-steps
+constexpr int kX6Row = 40;                   // bf16 per staged feature row (80 B)
+constexpr int kX6Piece = kTile * kX6Row;     // bf16 per (operand, piece) image
+
+__global__ void __launch_bounds__(256) pgemm_x6_kernel(const WgradJob* __restrict__ jobs,
+                                                       const int* __restrict__ prefix, int njobs,
+                                                       float* __restrict__ slab) {
+  __shared__ __attribute__((aligned(16))) unsigned short lds[2 * 3 * kX6Piece];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int j = find_job(prefix, njobs, blockIdx.x);
+  const WgradJob J = jobs[j];
+  int t = blockIdx.x - prefix[j];
+  const int split = t % J.splits;
+  t /= J.splits;
+  const int ti = t % J.tiles_i, to = t / J.tiles_i;
+  const int chunk = ((J.P + J.splits - 1) / J.splits + kX6Stage - 1) / kX6Stage * kX6Stage;
+  const long pb = (long)split * chunk;
+  const long pe = min((long)J.P, pb + chunk);
+  const int wo = wave >> 1, wi = wave & 1;      // 64x64 quadrant of this wave
+  const int r32 = lane & 31, h = lane >> 5;
+  const int f = tid & 127, g = tid >> 7;        // staging role: feature f, points 16g .. 16g+15
+  const int fo = to * kTile + f, fi = ti * kTile + f;
+  const bool fo_ok = fo < J.out, fi_ok = fi < J.in;
+  const bool want_db = (J.db != nullptr) && ti == 0;
+  const bool gel = J.x_gelu != 0;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{};
+  float dbacc = 0.f;
+
+  float ra[16], rb[16];
+  auto load_stage = [&](long pbase) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const long p = pbase + 16 * g + k;
+      const bool pv = p < pe;
+      ra[k] = (pv && fo_ok) ? J.dz[p * J.lddz + fo] : 0.f;
+      rb[k] = (pv && fi_ok) ? J.x[p * J.ldx + fi] : 0.f;
+    }
+  };
+
+  if (pb < pe) load_stage(pb);
+  for (long p0 = pb; p0 < pe; p0 += kX6Stage) {
+    __syncthreads();                          // previous stage fully consumed
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      float va[8], vb[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        va[k] = ra[8 * half + k];
+        vb[k] = gel ? gelu(rb[8 * half + k]) : rb[8 * half + k];
+        dbacc += va[k];
+      }
+      u32x4 pa[3], pbv[3];
+      split8_x6(va, pa);
+      split8_x6(vb, pbv);
+      const int col = 16 * g + 8 * half;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        *reinterpret_cast<u32x4*>(lds + q * kX6Piece + f * kX6Row + col) = pa[q];
+        *reinterpret_cast<u32x4*>(lds + (3 + q) * kX6Piece + f * kX6Row + col) = pbv[q];
+      }
+    }
+    __syncthreads();
+    if (p0 + kX6Stage < pe) load_stage(p0 + kX6Stage);   // in flight during the MFMAs
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int koff = 16 * ks + 8 * h;
+      u32x4 af[2][3], bf[2][3];
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+          af[a][q] = *reinterpret_cast<const u32x4*>(lds + q * kX6Piece + (wo * 64 + a * 32 + r32) * kX6Row + koff);
+          bf[a][q] = *reinterpret_cast<const u32x4*>(lds + (3 + q) * kX6Piece + (wi * 64 + a * 32 + r32) * kX6Row + koff);
+        }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+#define GNOT_MFMA32(X, Y, C) \
+  C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, X), __builtin_bit_cast(bf16x8, Y), C, 0, 0, 0)
+          // smallest terms first
+          GNOT_MFMA32(af[a][2], bf[b][0], acc[a][b]);
+          GNOT_MFMA32(af[a][1], bf[b][1], acc[a][b]);
+          GNOT_MFMA32(af[a][0], bf[b][2], acc[a][b]);
+          GNOT_MFMA32(af[a][1], bf[b][0], acc[a][b]);
+          GNOT_MFMA32(af[a][0], bf[b][1], acc[a][b]);
+          GNOT_MFMA32(af[a][0], bf[b][0], acc[a][b]);
+#undef GNOT_MFMA32
+        }
+    }
+  }
+
+  // partial tile -> slab [split][tile 128 x (128 + 1)] (same layout as pgemm_kernel)
+  const int ntile = J.tiles_o * J.tiles_i;
+  const int tile = to * J.tiles_i + ti;
+  float* S = slab + J.slab_off + ((long)split * ntile + tile) * (kTile * (kTile + 1));
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wo * 64 + a * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int col = wi * 64 + b * 32 + r32;
+        S[row * (kTile + 1) + col] = acc[a][b][r];
+      }
+  if (want_db) {
+    // column sums of A: the two point halves of every feature through LDS
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(lds);
+    red[tid] = dbacc;
+    __syncthreads();
+    if (g == 0) S[f * (kTile + 1) + kTile] = red[f] + red[128 + f];
+  }
+}
+
 // sum the split partials; normal jobs write dW[out, in] (+ db[out]); state jobs (state_dh > 0) write
 // the per-head diagonal blocks into [H][dh*dh + dh] (S row-major, then z)
 __global__ void __launch_bounds__(256) pgemm_reduce_kernel(const WgradJob* __restrict__ jobs,
@@ -220,9 +354,12 @@ __global__ void __launch_bounds__(256) pgemm_reduce_kernel(const WgradJob* __res
 }
 
 hipError_t launch_wgrad(const WgradJob* jobs_dev, const int* wg_prefix_dev, int njobs, int total_wgs,
-                        const int* red_prefix_dev, int total_red, float* slab, hipStream_t s) {
+                        const int* red_prefix_dev, int total_red, float* slab, hipStream_t s, bool x6) {
   if (njobs <= 0) return hipSuccess;
-  hipLaunchKernelGGL(pgemm_kernel, dim3(total_wgs), dim3(256), 0, s, jobs_dev, wg_prefix_dev, njobs, slab);
+  if (x6)
+    hipLaunchKernelGGL(pgemm_x6_kernel, dim3(total_wgs), dim3(256), 0, s, jobs_dev, wg_prefix_dev, njobs, slab);
+  else
+    hipLaunchKernelGGL(pgemm_kernel, dim3(total_wgs), dim3(256), 0, s, jobs_dev, wg_prefix_dev, njobs, slab);
   hipLaunchKernelGGL(pgemm_reduce_kernel, dim3((total_red + 255) / 256), dim3(256), 0, s, jobs_dev,
                      red_prefix_dev, njobs, total_red, (const float*)slab);
   return hipGetLastError();
