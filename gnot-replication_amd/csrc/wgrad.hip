@@ -178,14 +178,53 @@ __global__ void __launch_bounds__(256) pgemm_kernel(const WgradJob* __restrict__
 // like the forward chains; one accumulator per block keeps two workgroups per CU within the register
 // file): 6 x 32 = 192 matrix-pipe cycles per 32x32x16 block
 // instead of 8 x 64 = 512 on v_mfma_f32_32x32x2_f32.
-// Staging: thread (f = t & 127, g = t >> 7) loads feature f of 16 consecutive points (dword loads,
-// each wave-instruction reading 256 contiguous bytes of one row), so 8 consecutive points of one
-// feature are register-local and go to LDS as one 16-byte piece vector per piece: the LDS image is
-// [operand][piece][feature][point] with an 80-byte feature row (32 points + pad), which makes the
-// MFMA fragment read (lane = feature, 8 consecutive points) a conflict-free ds_read_b128.
+// Staging: thread (pair fp = t & 63, octet o = t >> 6 = its wave) loads features 2fp, 2fp+1 of the
+// stage's points 8o .. 8o+7 (one float2 per point: a wave reads whole 512-byte rows), so 8 consecutive
+// points of one feature are register-local and go to LDS as one 16-byte vector per piece.  The LDS
+// image is [operand][piece][feature][point] with an 80-byte feature row (32 points + pad): the MFMA
+// fragment read (lane = feature, 8 consecutive points) is a conflict-free ds_read_b128.
 constexpr int kX6Stage = 32;                 // points per stage = two 16-point MFMA k-steps
 constexpr int kX6Row = 40;                   // bf16 per staged feature row (80 B)
 constexpr int kX6Piece = kTile * kX6Row;     // bf16 per (operand, piece) image
+
+// global-address-space view of a job pointer (the pointers come from a job table, so the compiler
+// cannot infer it and would emit flat loads, which also count against lgkmcnt)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define GNOT_GLOBAL __attribute__((address_space(1)))
+#else
+#define GNOT_GLOBAL
+#endif
+typedef const float GNOT_GLOBAL* gfloat_ptr;
+typedef const float2 GNOT_GLOBAL* gfloat2_ptr;
+
+// 8 points x 2 features of one operand: v[j][k] = rows[p_k][f0 + j]; rows past `pe` and features
+// past `ncols` read as 0.  Edge path: clamped (always valid) addresses plus selects, no branches
+// per load; the row clamp is wave-uniform (prow is per wave).
+GNOT_DEV void x6_load8x2(float (&v)[2][8], const float* base, long ld, long prow, long pe, int f0, int ncols,
+                         bool full, bool vec) {
+  gfloat_ptr g = (gfloat_ptr)base;
+  if (full && vec) {
+    gfloat_ptr r = g + prow * ld + f0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float2 x = *(gfloat2_ptr)(r + k * ld);
+      v[0][k] = x.x;
+      v[1][k] = x.y;
+    }
+    return;
+  }
+  const int c0 = min(f0, ncols - 1), c1 = min(f0 + 1, ncols - 1);
+  const bool ok0 = f0 < ncols, ok1 = f0 + 1 < ncols;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const long p = min(prow + k, pe - 1);
+    const bool pv = prow + k < pe;
+    gfloat_ptr r = g + p * ld;
+    const float x0 = r[c0], x1 = r[c1];
+    v[0][k] = (pv && ok0) ? x0 : 0.f;
+    v[1][k] = (pv && ok1) ? x1 : 0.f;
+  }
+}
 
 __global__ void __launch_bounds__(256) pgemm_x6_kernel(const WgradJob* __restrict__ jobs,
                                                        const int* __restrict__ prefix, int njobs,
@@ -204,9 +243,11 @@ __global__ void __launch_bounds__(256) pgemm_x6_kernel(const WgradJob* __restric
   const long pe = min((long)J.P, pb + chunk);
   const int wo = wave >> 1, wi = wave & 1;      // 64x64 quadrant of this wave
   const int r32 = lane & 31, h = lane >> 5;
-  const int f = tid & 127, g = tid >> 7;        // staging role: feature f, points 16g .. 16g+15
-  const int fo = to * kTile + f, fi = ti * kTile + f;
-  const bool fo_ok = fo < J.out, fi_ok = fi < J.in;
+  const int fp = lane, o = wave;                // staging role
+  const int fo = to * kTile + 2 * fp, fi = ti * kTile + 2 * fp;
+  // float2 fast path: the whole tile inside the operand's columns and 8-byte aligned rows
+  const bool tile_a = to * kTile + kTile <= J.out && (J.lddz & 1) == 0 && (reinterpret_cast<size_t>(J.dz) & 7) == 0;
+  const bool tile_b = ti * kTile + kTile <= J.in && (J.ldx & 1) == 0 && (reinterpret_cast<size_t>(J.x) & 7) == 0;
   const bool want_db = (J.db != nullptr) && ti == 0;
   const bool gel = J.x_gelu != 0;
 
@@ -215,40 +256,37 @@ __global__ void __launch_bounds__(256) pgemm_x6_kernel(const WgradJob* __restric
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{};
-  float dbacc = 0.f;
+  float dbacc[2] = {0.f, 0.f};
 
-  float ra[16], rb[16];
+  float ra[2][8], rb[2][8];
   auto load_stage = [&](long pbase) {
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const long p = pbase + 16 * g + k;
-      const bool pv = p < pe;
-      ra[k] = (pv && fo_ok) ? J.dz[p * J.lddz + fo] : 0.f;
-      rb[k] = (pv && fi_ok) ? J.x[p * J.ldx + fi] : 0.f;
-    }
+    const long prow = pbase + 8 * o;
+    const bool full = prow + 7 < pe;
+    x6_load8x2(ra, J.dz, J.lddz, prow, pe, fo, J.out, full, tile_a);
+    x6_load8x2(rb, J.x, J.ldx, prow, pe, fi, J.in, full, tile_b);
   };
 
   if (pb < pe) load_stage(pb);
   for (long p0 = pb; p0 < pe; p0 += kX6Stage) {
     __syncthreads();                          // previous stage fully consumed
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      float va[8], vb[8];
+    for (int jf = 0; jf < 2; ++jf) {
+      float vb[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        va[k] = ra[8 * half + k];
-        vb[k] = gel ? gelu(rb[8 * half + k]) : rb[8 * half + k];
-        dbacc += va[k];
+        vb[k] = gel ? gelu(rb[jf][k]) : rb[jf][k];
+        dbacc[jf] += ra[jf][k];
       }
       u32x4 pa[3], pbv[3];
-      split8_x6(va, pa);
+      split8_x6(ra[jf], pa);
       split8_x6(vb, pbv);
-      const int col = 16 * g + 8 * half;
+      const int f = 2 * fp + jf;
 #pragma unroll
       for (int q = 0; q < 3; ++q) {
-        *reinterpret_cast<u32x4*>(lds + q * kX6Piece + f * kX6Row + col) = pa[q];
-        *reinterpret_cast<u32x4*>(lds + (3 + q) * kX6Piece + f * kX6Row + col) = pbv[q];
+        *reinterpret_cast<u32x4*>(lds + q * kX6Piece + f * kX6Row + 8 * o) = pa[q];
+        *reinterpret_cast<u32x4*>(lds + (3 + q) * kX6Piece + f * kX6Row + 8 * o) = pbv[q];
       }
+      asm volatile("" ::: "memory");          // one feature at a time: bounds the staging registers
     }
     __syncthreads();
     if (p0 + kX6Stage < pe) load_stage(p0 + kX6Stage);   // in flight during the MFMAs
@@ -278,6 +316,7 @@ __global__ void __launch_bounds__(256) pgemm_x6_kernel(const WgradJob* __restric
           GNOT_MFMA32(af[a][0], bf[b][0], acc[a][b]);
 #undef GNOT_MFMA32
         }
+      asm volatile("" ::: "memory");          // k-step 1's fragments are not hoisted over k-step 0
     }
   }
 
@@ -296,12 +335,13 @@ __global__ void __launch_bounds__(256) pgemm_x6_kernel(const WgradJob* __restric
         S[row * (kTile + 1) + col] = acc[a][b][r];
       }
   if (want_db) {
-    // column sums of A: the two point halves of every feature through LDS
+    // column sums of A: the four point octets of every feature through LDS, in a fixed order
     __syncthreads();
     float* red = reinterpret_cast<float*>(lds);
-    red[tid] = dbacc;
+    red[o * kTile + 2 * fp] = dbacc[0];
+    red[o * kTile + 2 * fp + 1] = dbacc[1];
     __syncthreads();
-    if (g == 0) S[f * (kTile + 1) + kTile] = red[f] + red[128 + f];
+    if (tid < kTile) S[tid * (kTile + 1) + kTile] = (red[tid] + red[kTile + tid]) + (red[2 * kTile + tid] + red[3 * kTile + tid]);
   }
 }
 
