@@ -471,14 +471,23 @@ static void plan_images(gnot_plan* p) {
 
 // ====================================================================== point-reduction GEMM groups
 static void finish_group(gnot_plan* p, WgradGroup& G) {
+  // env GNOT_WGRAD_FP32: weight gradients on the fp32 MFMA kernel (diagnostics)
+  static const bool fp32_only = std::getenv("GNOT_WGRAD_FP32") != nullptr;
+  G.x6 = !fp32_only;
+  for (const auto& J : G.jobs)
+    if (J.w != nullptr || J.state_dh > 0 || J.diag_only) G.x6 = false;
+  // the x6 kernel holds ~240 registers per lane: one workgroup per CU leaves the other half of
+  // every SIMD's register file to the concurrent main-stream kernels (env GNOT_X6_WGS overrides)
+  static const long x6_wgs = std::getenv("GNOT_X6_WGS") ? std::atol(std::getenv("GNOT_X6_WGS")) : 256;
+  const long target = G.x6 ? x6_wgs : kTargetWGs;
   long tiles = 0;
   for (auto& J : G.jobs) {
     J.tiles_o = (J.out + kPTile - 1) / kPTile;
     J.tiles_i = (J.in + kPTile - 1) / kPTile;
     tiles += J.diag_only ? J.tiles_o : J.tiles_o * J.tiles_i;
   }
-  // floor, not ceil: never more than kTargetWGs (= 2 per CU) workgroups, so no CU runs a third one
-  const long want = std::max<long>(1, kTargetWGs / std::max<long>(tiles, 1));
+  // floor, not ceil: never more than `target` workgroups, so no CU runs one more than planned
+  const long want = std::max<long>(1, target / std::max<long>(tiles, 1));
   G.wg_prefix.clear();
   G.red_prefix.clear();
   G.slab_floats = 0;
@@ -497,11 +506,6 @@ static void finish_group(gnot_plan* p, WgradGroup& G) {
   }
   G.total_wgs = wg;
   G.total_red = red;
-  // env GNOT_WGRAD_FP32: weight gradients on the fp32 MFMA kernel (diagnostics)
-  static const bool fp32_only = std::getenv("GNOT_WGRAD_FP32") != nullptr;
-  G.x6 = !fp32_only;
-  for (const auto& J : G.jobs)
-    if (J.w != nullptr || J.state_dh > 0 || J.diag_only) G.x6 = false;
   size_t& slab = (!G.jobs.empty() && G.jobs[0].state_dh > 0) ? p->slab_state_floats : p->slab_wgrad_floats;
   slab = std::max(slab, G.slab_floats);
 }
