@@ -62,6 +62,7 @@ struct WgradGroup {
   int total_wgs = 0, total_red = 0;
   size_t slab_floats = 0;
   bool x6 = false;                   // plain weight-gradient jobs: the bf16x6 MFMA kernel
+  int state_pts = 0, state_nw = 0;   // state groups: points per workgroup, per-point weights (0 or H)
   WgradJob* d_jobs = nullptr;        // device copies (workspace tables)
   int* d_wg_prefix = nullptr;
   int* d_red_prefix = nullptr;
@@ -512,13 +513,21 @@ static void finish_group(gnot_plan* p, WgradGroup& G) {
 
 // attention-state group (state.hip): one job per sample, ceil(P / kStatePts) partial states each
 static void finish_state_group(gnot_plan* p, WgradGroup& G) {
+  static const int env_pts = std::getenv("GNOT_STATE_PTS") ? std::atoi(std::getenv("GNOT_STATE_PTS")) : 0;
+  if (!G.jobs.empty()) {
+    const int d = G.jobs[0].out;
+    G.state_pts = env_pts > 0 ? std::min(env_pts, 8192 / d) : state_pts(d);
+    G.state_nw = 0;
+    for (const auto& J : G.jobs)
+      if (J.w != nullptr) G.state_nw = d / J.state_dh;
+  }
   G.wg_prefix.clear();
   G.red_prefix.clear();
   G.slab_floats = 0;
   int wg = 0, red = 0;
   for (auto& J : G.jobs) {
     const int per = J.out / J.state_dh * (J.state_dh * J.state_dh + J.state_dh);
-    J.splits = std::max(1, (J.P + state_pts(J.out) - 1) / state_pts(J.out));
+    J.splits = std::max(1, (J.P + G.state_pts - 1) / G.state_pts);
     J.slab_off = (long)G.slab_floats;
     G.slab_floats += (size_t)J.splits * per;
     G.wg_prefix.push_back(wg);
@@ -1301,7 +1310,7 @@ int run_state(Ctx& c, const WgradGroup& G) {
   if (G.jobs.empty()) return GNOT_OK;
   ProfScope ps(c, "state", group_flops(G));
   GNOT_CK(launch_state(G.d_jobs, G.d_wg_prefix, (int)G.jobs.size(), G.total_wgs, G.d_red_prefix,
-                       G.total_red, c.p->P_("slab_state"), c.s));
+                       G.total_red, c.p->P_("slab_state"), G.jobs[0].out, G.state_pts, G.state_nw, c.s));
   return GNOT_OK;
 }
 

@@ -110,9 +110,12 @@ hipError_t launch_wgrad(const WgradJob* jobs_dev, const int* wg_prefix_dev, int 
 // Jobs are WgradJobs with state_dh > 0: A = dz/lddz, B = x/ldx, optional w/ldw, out = dW as
 // [H][dh*dh + dh], `splits` partials of state_pts(d) points each at slab + slab_off.
 // points per partial state: the workgroup's A and B rows fill <= 32 KiB of LDS each
-inline __host__ __device__ int state_pts(int d) { return d <= 128 ? 64 : 8192 / d; }
+// points per partial-state workgroup (64 at d <= 128, 8192 / d above; measured: 32 and 16 are slower
+// at cfg2); env GNOT_STATE_PTS overrides
+inline int state_pts(int d) { return d <= 128 ? 64 : 8192 / d; }
 hipError_t launch_state(const WgradJob* jobs_dev, const int* wg_prefix_dev, int njobs, int total_wgs,
-                        const int* red_prefix_dev, int total_red, float* slab, hipStream_t s);
+                        const int* red_prefix_dev, int total_red, float* slab, int d, int pts, int nw,
+                        hipStream_t s);   // d: row width, pts: points per workgroup, nw: per-point weights (0 or H)
 
 // ------------------------------------------------------------------ attention (attn.hip)
 struct AttnApplyArgs {

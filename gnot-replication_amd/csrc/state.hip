@@ -38,13 +38,12 @@ constexpr int kMaxBlk = 4;   // 4x4 output blocks per thread: H*(dh/4)^2 <= 1024
 // A region, reused) and the workgroup's partial state goes to the slab.
 __global__ void __launch_bounds__(kStateThreads) state_partial_kernel(const WgradJob* __restrict__ jobs,
                                                                      const int* __restrict__ prefix, int njobs,
-                                                                     float* __restrict__ slab) {
+                                                                     float* __restrict__ slab, int pts) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int j = find_job_s(prefix, njobs, blockIdx.x);
   const WgradJob& J = jobs[j];
   const int split = blockIdx.x - prefix[j];
   const int dh = J.state_dh, d = J.out, H = d / dh, nb = dh / 4;
-  const int pts = state_pts(d);
   const int nblk = H * nb * nb;
   const int per = H * (dh * dh + dh);
   const long p0 = (long)split * pts;
@@ -176,18 +175,20 @@ __global__ void __launch_bounds__(256) state_reduce_kernel(const WgradJob* __res
 }
 
 hipError_t launch_state(const WgradJob* jobs_dev, const int* wg_prefix_dev, int njobs, int total_wgs,
-                        const int* red_prefix_dev, int total_red, float* slab, hipStream_t s) {
+                        const int* red_prefix_dev, int total_red, float* slab, int d, int pts, int nw,
+                        hipStream_t s) {
   if (njobs <= 0 || total_wgs <= 0) return hipSuccess;
-  // dynamic LDS: A and B stages (state_pts(d) * d floats each, <= 32 KiB) + weights (<= 64 x 64 floats)
-  const size_t lds = (2 * 8192 + 64 * 64) * sizeof(float);
+  // dynamic LDS, exactly what the workgroup stages: A and B rows (pts * d floats each) + the
+  // per-(point, head) weights; the partial-state combine reuses the A/B region (256 x 20 floats)
+  const size_t lds = std::max<size_t>((size_t)(2 * pts * d + pts * nw), 256 * 20) * sizeof(float);
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(state_partial_kernel),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)((2 * 8192 + 64 * 64) * sizeof(float)));
     attr = true;
   }
   hipLaunchKernelGGL(state_partial_kernel, dim3(total_wgs), dim3(kStateThreads), lds, s, jobs_dev, wg_prefix_dev,
-                     njobs, slab);
+                     njobs, slab, pts);
   hipLaunchKernelGGL(state_reduce_kernel, dim3((total_red * 8 + 255) / 256), dim3(256), 0, s, jobs_dev, red_prefix_dev,
                      njobs, total_red, (const float*)slab);
   return hipGetLastError();
