@@ -1502,17 +1502,9 @@ extern "C" int gnot_forward(gnot_plan* p, const float* x, const float* theta, co
   const long P = p->P;
   const int D = p->D, E = p->E, NL = p->NL;
   const bool tr = p->training;
-  // inputs into the workspace (row pitch rounded to 16 B)
-  GNOT_CK(hipMemcpy2DAsync(p->P_("x"), p->bufs["x"].ld * 4, x, p->in * 4, p->in * 4, P, hipMemcpyDeviceToDevice, c.s));
-  GNOT_CK(hipMemcpyAsync(p->P_("theta"), theta, (size_t)p->B * p->th * 4, hipMemcpyDeviceToDevice, c.s));
-  for (int i = 0; i < p->I; ++i) {
-    const std::string n = "fn" + std::to_string(i);
-    if (p->Q[i] > 0)
-      GNOT_CK(hipMemcpy2DAsync(p->P_(n), p->bufs[n].ld * 4, fns[i], p->F * 4, p->F * 4, p->Q[i],
-                               hipMemcpyDeviceToDevice, c.s));
-  }
   // the input-function branch (encoders, every block's K/V projections and states) depends only on
-  // the input functions: it runs on side2 while the query branch (gating, x encoder) runs here
+  // the input functions: it runs on side2 while the query branch (gating, x encoder) runs here.  The
+  // query branch is issued first (graph replay dispatches in capture order).
   static const bool no_fwd2 = std::getenv("GNOT_NO_SIDE2_FWD") != nullptr;
   const bool br = p->I > 0 && !no_fwd2;
   Ctx cf{p, br ? p->side2 : c.s};
@@ -1521,23 +1513,9 @@ extern "C" int gnot_forward(gnot_plan* p, const float* x, const float* theta, co
     GNOT_CK(hipEventRecord(fork, c.s));
     GNOT_CK(hipStreamWaitEvent(cf.s, fork, 0));
   }
-  // input-function encoders (model.py:164-166)
-  for (int i = 0; i < p->I; ++i) {
-    const std::string si = std::to_string(i);
-    ChainArgs a = chain_args(p, p->ch_fn[i], p->Q[i]);
-    a.X = p->P_("fn" + si); a.ldx = p->bufs["fn" + si].ld;
-    a.Y = p->P_("fnenc" + si); a.ldy = D; a.mode = CH_STORE;
-    if (tr) { a.save = p->P_("fn_save" + si); a.save_layer_stride = p->Q[i] * D; a.save_chain_stride = NL * p->Q[i] * D; }
-    GNOT_CK(launch_chain_fwd(a, cf.s));
-  }
-  // key/value projections (model.py:67-75) and states (model.py:77-79) of every (block, input
-  // function): they depend only on the input-function encodings, so all L*I of them run batched here
-  if (p->I > 0 && p->L > 0) {
-    long Qmax = 0;
-    for (long q : p->Q) Qmax = std::max(Qmax, q);
-    GNOT_CK(launch_linear_batch(p->d_fwd_kv_jobs, (int)p->fwd_kv_jobs.size(), (int)Qmax, 2 * D, D, cf.s));
-    GNOT_RUN(run_state(cf, p->st_fn));
-  }
+  // inputs into the workspace (row pitch rounded to 16 B)
+  GNOT_CK(hipMemcpy2DAsync(p->P_("x"), p->bufs["x"].ld * 4, x, p->in * 4, p->in * 4, P, hipMemcpyDeviceToDevice, c.s));
+  GNOT_CK(hipMemcpyAsync(p->P_("theta"), theta, (size_t)p->B * p->th * 4, hipMemcpyDeviceToDevice, c.s));
   GNOT_CK(launch_concat_theta(p->P_("x"), p->bufs["x"].ld, p->in, p->P_("theta"), p->th, p->d_xoff, p->B,
                               p->P_("xin"), p->bufs["xin"].ld, (int)P, c.s));
   // gating (model.py:155-156)
@@ -1555,6 +1533,29 @@ extern "C" int gnot_forward(gnot_plan* p, const float* x, const float* theta, co
     a.Y = p->P_("query0"); a.ldy = D; a.mode = CH_STORE;
     if (tr) { a.save = p->P_("x_save"); a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D; }
     GNOT_CK(launch_chain_fwd(a, c.s));
+  }
+  for (int i = 0; i < p->I; ++i) {
+    const std::string n = "fn" + std::to_string(i);
+    if (p->Q[i] > 0)
+      GNOT_CK(hipMemcpy2DAsync(p->P_(n), p->bufs[n].ld * 4, fns[i], p->F * 4, p->F * 4, p->Q[i],
+                               hipMemcpyDeviceToDevice, cf.s));
+  }
+  // input-function encoders (model.py:164-166)
+  for (int i = 0; i < p->I; ++i) {
+    const std::string si = std::to_string(i);
+    ChainArgs a = chain_args(p, p->ch_fn[i], p->Q[i]);
+    a.X = p->P_("fn" + si); a.ldx = p->bufs["fn" + si].ld;
+    a.Y = p->P_("fnenc" + si); a.ldy = D; a.mode = CH_STORE;
+    if (tr) { a.save = p->P_("fn_save" + si); a.save_layer_stride = p->Q[i] * D; a.save_chain_stride = NL * p->Q[i] * D; }
+    GNOT_CK(launch_chain_fwd(a, cf.s));
+  }
+  // key/value projections (model.py:67-75) and states (model.py:77-79) of every (block, input
+  // function): they depend only on the input-function encodings, so all L*I of them run batched here
+  if (p->I > 0 && p->L > 0) {
+    long Qmax = 0;
+    for (long q : p->Q) Qmax = std::max(Qmax, q);
+    GNOT_CK(launch_linear_batch(p->d_fwd_kv_jobs, (int)p->fwd_kv_jobs.size(), (int)Qmax, 2 * D, D, cf.s));
+    GNOT_RUN(run_state(cf, p->st_fn));
   }
   if (br) {                                // join the input-function branch
     hipEvent_t join = next_event(p);
