@@ -22,8 +22,11 @@ namespace gnot {
 // for twice the L2->LDS weight traffic.
 constexpr int kChainWaves = 4;
 
+// 3 waves per SIMD (<= 168 VGPRs + AGPRs) at d <= 128: a 10k-point MoE launch (2,500 waves) is then
+// ONE round on the 1,024 SIMDs instead of a full round plus a 20 % tail round at 2 waves per SIMD
 template <int D, int KT0, int OTL>
-__global__ void __launch_bounds__(64 * kChainWaves) chain_fwd_kernel(ChainArgs a) {
+__global__ void __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_eu(D <= 128 ? 3 : 1)))
+chain_fwd_kernel(ChainArgs a) {
   constexpr int DT = D / 16;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;

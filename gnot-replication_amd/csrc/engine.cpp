@@ -387,7 +387,7 @@ static void plan_images(gnot_plan* p) {
     J.out = p->lin_o[li];
     J.in = p->lin_i[li];
     J.transposed = tr;
-    J.o0 = o0; J.t0 = t0; J.ktot = im.KT;
+    J.o0 = o0; J.t0 = t0; J.ktot = im.KT; J.otot = im.OT;
     J.OTp = OTp; J.KTp = KTp;
     p->pack_jobs.push_back(J);
     p->pack_dst_off4.push_back(im.off4);

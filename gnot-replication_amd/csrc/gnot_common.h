@@ -257,24 +257,37 @@ GNOT_DEV void mm_tiles_pipe(const float4* __restrict__ Wg, const float4* __restr
 //
 // Point form carries over unchanged: for k-block t (features 32t..32t+31) lane (p, g) feeds MFMA
 // k-slots 8g+j with its own registers: j < 4 -> feature 32t+4g+j (tile 2t), j >= 4 -> feature
-// 32t+16+4g+(j-4) (tile 2t+1).  Weight images (pack.hip, x6 jobs) use the same k order:
-// image[((o*KB + t)*3 + q)*64 + lane] = 8 bf16 of piece q of rows 16o+(lane&15), k-slots 8(lane>>4)+j.
+// 32t+16+4g+(j-4) (tile 2t+1).  Weight images (pack.hip, x6 jobs) use the same k order, k-major:
+// image[((t*OT + o)*3 + q)*64 + lane] = 8 bf16 of piece q of rows 16o+(lane&15), k-slots 8(lane>>4)+j.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-// LDS buffer of the bf16x6 weight stream: at least one output tile's full-K image (ceil(DT/2)*3 KiB);
-// 24 KiB per buffer (measured at d = 128: 12 KiB buffers, 6 instead of 3 workgroups per CU, are slower)
+// LDS buffer of the bf16x6 weight stream: 24 KiB per buffer, double-buffered.
+// Images are k-MAJOR: block (t, o) = output tile o, k-block t (32 contraction slots) at
+//   image[((t*OT + o)*3 + q)*64 + lane]
+// so a chunk is TCH whole k-blocks (all OT output tiles) or, when one k-block of all tiles exceeds the
+// buffer (d = 256), OCH output tiles of one k-block.  Consuming a layer k-block by k-block means only
+// the current block's three B pieces are live (12 VGPRs instead of 12*ceil(KT/2)), which with a
+// single accumulator set keeps the d = 128 forward chain at 3 waves per SIMD.
 constexpr int x6_buf_kb(int) { return 24; }
 constexpr int x6_buf_f4(int D) { return x6_buf_kb(D) * WAVE; }   // 16-byte units per buffer
 
 template <int D>
-constexpr int x6_och(int KT, int OT) {                // output tiles per chunk (KB*3 KiB per tile)
+constexpr int x6_och(int KT, int OT) {                // output tiles per chunk (3 KiB per block)
   int c = OT;
-  while (c > 1 && (c * ((KT + 1) / 2) * 3 > x6_buf_kb(D) || OT % c != 0)) --c;
+  while (c > 1 && (c * 3 > x6_buf_kb(D) || OT % c != 0)) --c;
   return c;
 }
 template <int D>
-constexpr int x6_chunk_f4(int KT, int OT) { return x6_och<D>(KT, OT) * ((KT + 1) / 2) * 3 * WAVE; }
+constexpr int x6_tch(int KT, int OT) {                // k-blocks per chunk
+  const int KB = (KT + 1) / 2;
+  if (x6_och<D>(KT, OT) != OT) return 1;
+  int c = KB;
+  while (c > 1 && (c * OT * 3 > x6_buf_kb(D) || KB % c != 0)) --c;
+  return c;
+}
+template <int D>
+constexpr int x6_chunk_f4(int KT, int OT) { return x6_och<D>(KT, OT) * x6_tch<D>(KT, OT) * 3 * WAVE; }
 
 GNOT_DEV unsigned f2u(float x) { return __builtin_bit_cast(unsigned, x); }
 GNOT_DEV float u2f(unsigned x) { return __builtin_bit_cast(float, x); }
@@ -301,22 +314,16 @@ GNOT_DEV void split8_x6(const float (&v)[8], u32x4 (&p)[3]) {
   }
 }
 
-// B pieces of the point-form activations in[KT][4]: bp[q][t] = 8 bf16 (4 dwords) of piece q, block t
+// B pieces of k-block t of the point-form activations in[KT][4]: bp[q] = 8 bf16 (4 dwords) of piece q
 template <int KT>
-GNOT_DEV void split_x6(const float (&in)[KT][4], u32x4 (&bp)[3][(KT + 1) / 2]) {
+GNOT_DEV void split_block_x6(const float (&in)[KT][4], int t, u32x4 (&bp)[3]) {
+  float v[8];
 #pragma unroll
-  for (int t = 0; t < (KT + 1) / 2; ++t) {
-    float v[8];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      v[j] = in[2 * t][j];
-      v[4 + j] = (2 * t + 1 < KT) ? in[2 * t + 1][j] : 0.f;
-    }
-    u32x4 p[3];
-    split8_x6(v, p);
-#pragma unroll
-    for (int q = 0; q < 3; ++q) bp[q][t] = p[q];
+  for (int j = 0; j < 4; ++j) {
+    v[j] = in[2 * t][j];
+    v[4 + j] = (2 * t + 1 < KT) ? in[2 * t + 1][j] : 0.f;
   }
+  split8_x6(v, bp);
 }
 
 GNOT_DEV f32x4 mfma_bf16(const u32x4& a, const u32x4& b, f32x4 c) {
@@ -325,55 +332,54 @@ GNOT_DEV f32x4 mfma_bf16(const u32x4& a, const u32x4& b, f32x4 c) {
 }
 
 // Same contract as mm_tiles_pipe (acc pre-initialised, chunks double-buffered in `lds` of
-// 2*kChunkX6F4 units, next image staged across the layer boundary, hook on the last chunk), for
-// x6 weight images.  acc gets the order-0 term; the order-1/2 terms accumulate in a second set of
-// accumulators that is added at the end.
+// 2*x6_buf_f4 units, next image staged across the layer boundary, hook after the first chunk's
+// barrier), for k-major x6 weight images.  Per 16x16x32 block the six order <= 2 products go into
+// the tile's one accumulator, smallest terms first (a single accumulation chain of
+// v_mfma_f32_16x16x32_bf16 issues at full rate, MI355X_MICROARCH.md).
 template <int D, int KT, int OT, typename Hook = NoHook>
 GNOT_DEV void mm_tiles_pipe_x6(const float4* __restrict__ Wg, const float4* __restrict__ next_W, int next_f4,
                                float4* lds, int& cnt, const float (&in)[KT][4], f32x4 (&acc)[OT], int nwaves,
                                int wave, int lane, Hook hook = Hook()) {
-  constexpr int kChunkX6F4 = x6_buf_f4(D);
+  constexpr int kBufF4 = x6_buf_f4(D);
   constexpr int KB = (KT + 1) / 2;
   constexpr int OCH = x6_och<D>(KT, OT);
-  constexpr int NC = OT / OCH;
-  constexpr int CH4 = OCH * KB * 3 * WAVE;
-  u32x4 bp[3][KB];
-  split_x6<KT>(in, bp);
-  f32x4 lo[OT];
+  constexpr int TCH = x6_tch<D>(KT, OT);
+  constexpr int NOG = OT / OCH;
+  constexpr int NTG = KB / TCH;
+  constexpr int CH4 = OCH * TCH * 3 * WAVE;
 #pragma unroll
-  for (int o = 0; o < OT; ++o) lo[o] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int tg = 0; tg < NTG; ++tg) {
+    u32x4 bp[TCH][3];
 #pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    __syncthreads();
-    float4* nb = lds + ((cnt + 1) & 1) * kChunkX6F4;
-    if (c + 1 < NC) stage_image(nb, Wg + (c + 1) * CH4, CH4, nwaves, wave, lane);
-    else if (next_W) stage_image(nb, next_W, next_f4, nwaves, wave, lane);
-    if (c == 0) hook();
-    const u32x4* cb = reinterpret_cast<const u32x4*>(lds + (cnt & 1) * kChunkX6F4);
+    for (int tt = 0; tt < TCH; ++tt) split_block_x6<KT>(in, tg * TCH + tt, bp[tt]);
 #pragma unroll
-    for (int t = 0; t < KB; ++t) {
-      u32x4 a[OCH][3];
+    for (int og = 0; og < NOG; ++og) {
+      const int c = tg * NOG + og;
+      __syncthreads();
+      float4* nb = lds + ((cnt + 1) & 1) * kBufF4;
+      if (c + 1 < NTG * NOG) stage_image(nb, Wg + (c + 1) * CH4, CH4, nwaves, wave, lane);
+      else if (next_W) stage_image(nb, next_W, next_f4, nwaves, wave, lane);
+      if (c == 0) hook();
+      const u32x4* cb = reinterpret_cast<const u32x4*>(lds + (cnt & 1) * kBufF4);
 #pragma unroll
-      for (int o = 0; o < OCH; ++o)
+      for (int tt = 0; tt < TCH; ++tt)
 #pragma unroll
-        for (int q = 0; q < 3; ++q) a[o][q] = cb[((o * KB + t) * 3 + q) * WAVE + lane];
+        for (int o = 0; o < OCH; ++o) {
+          u32x4 a[3];
 #pragma unroll
-      for (int o = 0; o < OCH; ++o) acc[c * OCH + o] = mfma_bf16(a[o][0], bp[0][t], acc[c * OCH + o]);
-#pragma unroll
-      for (int o = 0; o < OCH; ++o) {
-        f32x4 l = lo[c * OCH + o];
-        l = mfma_bf16(a[o][0], bp[1][t], l);
-        l = mfma_bf16(a[o][1], bp[0][t], l);
-        l = mfma_bf16(a[o][0], bp[2][t], l);
-        l = mfma_bf16(a[o][1], bp[1][t], l);
-        l = mfma_bf16(a[o][2], bp[0][t], l);
-        lo[c * OCH + o] = l;
-      }
+          for (int q = 0; q < 3; ++q) a[q] = cb[((tt * OCH + o) * 3 + q) * WAVE + lane];
+          f32x4 r = acc[og * OCH + o];
+          r = mfma_bf16(a[2], bp[tt][0], r);
+          r = mfma_bf16(a[1], bp[tt][1], r);
+          r = mfma_bf16(a[0], bp[tt][2], r);
+          r = mfma_bf16(a[1], bp[tt][0], r);
+          r = mfma_bf16(a[0], bp[tt][1], r);
+          r = mfma_bf16(a[0], bp[tt][0], r);
+          acc[og * OCH + o] = r;
+        }
+      ++cnt;
     }
-    ++cnt;
   }
-#pragma unroll
-  for (int o = 0; o < OT; ++o) acc[o] += lo[o];
 }
 
 template <int OT>

@@ -21,7 +21,8 @@ struct PackJob {
   int transposed;
   int o0, t0, ktot;
   int OTp, KTp;        // tile counts of this job's image (>= what out/in need; the rest is zero)
-  int x6;              // 1: bf16x6 image (3 bf16 pieces per 16x32 block, gnot_common.h), else fp32
+  int x6;              // 1: bf16x6 image (3 bf16 pieces per 16x32 block, k-major, gnot_common.h), else fp32
+  int otot;            // x6: output tiles of the whole image (its k-major block stride)
 };
 // pack tiles of a job: fp32 images have OTp*KTp tiles, x6 images OTp*ceil(KTp/2) blocks
 inline int pack_tiles(const PackJob& J) { return J.x6 ? J.OTp * ((J.KTp + 1) / 2) : J.OTp * J.KTp; }
