@@ -205,10 +205,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs for the multi-process path on a one-GPU box (the real run is RCCL, one GPU per
+    # rank): GNOT_BENCH_BACKEND=gloo (host-staged collectives) and GNOT_BENCH_ONE_GPU=1 (every rank on
+    # cuda:0)
+    backend = os.environ.get("GNOT_BENCH_BACKEND", "nccl")
+    if os.environ.get("GNOT_BENCH_ONE_GPU"):
+        local = 0
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
