@@ -1554,7 +1554,7 @@ extern "C" int gnot_forward(gnot_plan* p, const float* x, const float* theta, co
   if (p->I > 0 && p->L > 0) {
     long Qmax = 0;
     for (long q : p->Q) Qmax = std::max(Qmax, q);
-    GNOT_CK(launch_linear_batch(p->d_fwd_kv_jobs, (int)p->fwd_kv_jobs.size(), (int)Qmax, 2 * D, D, cf.s));
+    GNOT_CK(launch_linear_batch(p->d_fwd_kv_jobs, (int)p->fwd_kv_jobs.size(), (int)Qmax, 2 * D, D, p->dh, cf.s));
     GNOT_RUN(run_state(cf, p->st_fn));
   }
   if (br) {                                // join the input-function branch
@@ -1676,7 +1676,7 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
     }
     GNOT_CK(launch_attn_kv_bwd_batch(p->d_kvbwd_jobs, (int)p->kvbwd_jobs.size(), maxch, p->H, p->dh, cf.s));
     for (size_t k = 0; k < p->d_dfn_jobs.size(); ++k)
-      GNOT_CK(launch_linear_batch(p->d_dfn_jobs[k], p->I, (int)Qmax, D, D, cf.s));
+      GNOT_CK(launch_linear_batch(p->d_dfn_jobs[k], p->I, (int)Qmax, D, D, p->dh, cf.s));
     GNOT_RUN(run_wgrad_side(cf, p->wg_fnkv, {}));
   }
   if (p->I > 0 && p->L == 0)   // encodings unused by the output: zero gradients

@@ -51,7 +51,7 @@ struct LinearArgs {
 };
 hipError_t launch_linear(const LinearArgs& a, int D, hipStream_t s);
 // jobs_dev: device array of independent LinearArgs (same D and NO), one per grid.z
-hipError_t launch_linear_batch(const LinearArgs* jobs_dev, int njobs, int maxP, int NO, int D, hipStream_t s);
+hipError_t launch_linear_batch(const LinearArgs* jobs_dev, int njobs, int maxP, int NO, int D, int dh, hipStream_t s);
 
 // ------------------------------------------------------------------ fused MLP chains (chain.hip)
 enum ChainMode { CH_STORE = 0, CH_SOFTMAX = 1, CH_MOE = 2 };

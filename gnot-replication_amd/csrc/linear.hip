@@ -10,15 +10,16 @@
 // weight images (backward-data of the q/k/v projections: dX = dQ Wq + dK Wk + dV Wv in one pass).
 // A batched variant runs independent jobs (e.g. the key/value projections of every block and
 // input function) in one launch.
+#include <cstdlib>
+
 #include "gnot_common.h"
 #include "gnot_kernels.h"
 
 namespace gnot {
 
-template <int D>
+template <int D, int OC>   // OC: output tiles per workgroup (grid.y splits NO)
 GNOT_DEV void linear_body(const LinearArgs& a, float4* wlds) {
   constexpr int KT = D / 16;
-  constexpr int OC = (D / 16) < 4 ? (D / 16) : 4;   // output tiles per workgroup (grid.y splits NO)
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const long p = ((long)blockIdx.x * 4 + wave) * 16 + (lane & 15);
@@ -73,53 +74,73 @@ GNOT_DEV void linear_body(const LinearArgs& a, float4* wlds) {
   store_rows<OC>(h, Y, a.ldy, p, valid, 16 * OC, lane);
 }
 
-template <int D>
+template <int D, int OC>
 __global__ void __launch_bounds__(256) linear_kernel(LinearArgs a) {
   __shared__ __attribute__((aligned(16))) float4 wlds[2 * kChunkF4];
-  linear_body<D>(a, wlds);
+  linear_body<D, OC>(a, wlds);
 }
 
 // several independent projections in one launch: job = blockIdx.z (jobs live in device memory)
-template <int D>
+template <int D, int OC>
 __global__ void __launch_bounds__(256) linear_batch_kernel(const LinearArgs* __restrict__ jobs) {
   __shared__ __attribute__((aligned(16))) float4 wlds[2 * kChunkF4];
   const LinearArgs a = jobs[blockIdx.z];
   if ((long)blockIdx.x * 64 >= a.P) return;        // whole workgroup: no barrier is skipped unevenly
-  linear_body<D>(a, wlds);
+  linear_body<D, OC>(a, wlds);
 }
 
-static int linear_nchunks(int D, int NO) {
-  const int oc = (D / 16) < 4 ? (D / 16) : 4;   // == linear_body's OC
-  return NO / (16 * oc);
+// Output tiles per workgroup.  Fewer tiles per wave means more waves per launch (a 10k-point d=128
+// projection is ~1,250 waves at 4 tiles, 2,500 at 2), but the input rows are re-read once per chunk
+// and the extra waves compete with the side-stream weight-gradient GEMMs: measured at cfg2, 4 tiles
+// 3.57 ms/step, 8 tiles 3.74, 2 tiles 3.75, 1 tile 4.00.
+// GNOT_LINEAR_OC overrides the choice (experiments); a choice that does not tile D and NO, or that
+// would split a softmax head (dh > 16 * oc), falls back to the widest valid one.
+static int linear_oc(int D, int NO, int nsoft, int dh) {
+  static const int env = [] {
+    const char* e = getenv("GNOT_LINEAR_OC");
+    return e ? atoi(e) : 0;
+  }();
+  const int kt = D / 16;
+  auto ok = [&](int oc) {
+    return oc >= 1 && oc <= 8 && kt % oc == 0 && NO % (16 * oc) == 0 && (nsoft == 0 || dh <= 16 * oc);
+  };
+  int want = env > 0 ? env : 4;
+  if (ok(want)) return want;
+  for (int oc = 8; oc >= 1; --oc)
+    if (ok(oc)) return oc;
+  return 1;
 }
+
+#define GNOT_LIN_CASES                                                                          \
+  GNOT_LIN(32, 1) GNOT_LIN(32, 2) GNOT_LIN(48, 1) GNOT_LIN(48, 3) GNOT_LIN(64, 1) GNOT_LIN(64, 2) \
+  GNOT_LIN(64, 4) GNOT_LIN(128, 1) GNOT_LIN(128, 2) GNOT_LIN(128, 4) GNOT_LIN(128, 8) GNOT_LIN(256, 1)             \
+  GNOT_LIN(256, 2) GNOT_LIN(256, 4) GNOT_LIN(256, 8)
 
 hipError_t launch_linear(const LinearArgs& a, int D, hipStream_t s) {
   if (a.P <= 0) return hipSuccess;
   if (a.nseg < 1 || a.nseg > kMaxSeg) return hipErrorInvalidValue;
-  const dim3 grid((a.P + 63) / 64, linear_nchunks(D, a.NO)), block(256);
-  switch (D) {
-    case 32: hipLaunchKernelGGL(linear_kernel<32>, grid, block, 0, s, a); break;
-    case 48: hipLaunchKernelGGL(linear_kernel<48>, grid, block, 0, s, a); break;
-    case 64: hipLaunchKernelGGL(linear_kernel<64>, grid, block, 0, s, a); break;
-    case 128: hipLaunchKernelGGL(linear_kernel<128>, grid, block, 0, s, a); break;
-    case 256: hipLaunchKernelGGL(linear_kernel<256>, grid, block, 0, s, a); break;
-    default: return hipErrorInvalidValue;
-  }
-  return hipGetLastError();
+  const int oc = linear_oc(D, a.NO, a.nsoft, a.dh);
+  const dim3 grid((a.P + 63) / 64, a.NO / (16 * oc)), block(256);
+#define GNOT_LIN(DD, OO) \
+  if (D == DD && oc == OO) { hipLaunchKernelGGL((linear_kernel<DD, OO>), grid, block, 0, s, a); return hipGetLastError(); }
+  GNOT_LIN_CASES
+#undef GNOT_LIN
+  return hipErrorInvalidValue;
 }
 
-hipError_t launch_linear_batch(const LinearArgs* jobs_dev, int njobs, int maxP, int NO, int D, hipStream_t s) {
+// jobs may carry a softmax epilogue: the tile choice keeps whole heads (dh) in one workgroup
+hipError_t launch_linear_batch(const LinearArgs* jobs_dev, int njobs, int maxP, int NO, int D, int dh, hipStream_t s) {
   if (njobs <= 0 || maxP <= 0) return hipSuccess;
-  const dim3 grid((maxP + 63) / 64, linear_nchunks(D, NO), njobs), block(256);
-  switch (D) {
-    case 32: hipLaunchKernelGGL(linear_batch_kernel<32>, grid, block, 0, s, jobs_dev); break;
-    case 48: hipLaunchKernelGGL(linear_batch_kernel<48>, grid, block, 0, s, jobs_dev); break;
-    case 64: hipLaunchKernelGGL(linear_batch_kernel<64>, grid, block, 0, s, jobs_dev); break;
-    case 128: hipLaunchKernelGGL(linear_batch_kernel<128>, grid, block, 0, s, jobs_dev); break;
-    case 256: hipLaunchKernelGGL(linear_batch_kernel<256>, grid, block, 0, s, jobs_dev); break;
-    default: return hipErrorInvalidValue;
+  const int oc = linear_oc(D, NO, 1, dh);
+  const dim3 grid((maxP + 63) / 64, NO / (16 * oc), njobs), block(256);
+#define GNOT_LIN(DD, OO)                                                                     \
+  if (D == DD && oc == OO) {                                                                 \
+    hipLaunchKernelGGL((linear_batch_kernel<DD, OO>), grid, block, 0, s, jobs_dev);          \
+    return hipGetLastError();                                                                \
   }
-  return hipGetLastError();
+  GNOT_LIN_CASES
+#undef GNOT_LIN
+  return hipErrorInvalidValue;
 }
 
 }  // namespace gnot
