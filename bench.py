@@ -5,23 +5,26 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-Workload (default) = BASELINE.json configs[1] (the metric's single-GPU configuration): GNOT with 4
-blocks, 4 experts, hidden 128, 8 heads, 4-layer MLPs, 2 input functions (multi-input cross-attention),
-one 2-D irregular mesh of 10,000 query points per GPU with 805 points per input function, fp32 (the
-reference computes in fp32).  A step = pack weights -> GNOT forward (gnot_amd, HIP) -> RelL2 loss
-(loss.py:14-23, per-sample segment sums) -> backward to every parameter gradient -> (N>1: one RCCL
-all-reduce of the flat gradient buffer) -> AdamW step.  Default multi-GPU scaling is weak: every rank
-owns its own mesh (SURVEY.md §8e sample-DP).  Other configs (--workload): cfg1 = configs[0] (main.py
-widths, batch 4 x 4096), cfg3 = configs[2] (256k-point 3-D mesh, d=256, 8 experts), cfg4 = configs[3]
-(ONE 1M-point mesh point-sharded over the ranks: strong scaling), cfg5 = configs[4] (64 variable
-meshes, LPT sample-DP).  --points / --meshes shrink them to fit fewer GPUs.
+Default workload = BASELINE.json configs[2], the largest configuration that fits one GPU: a synthetic
+3-D mesh of 262,144 query points, GNOT with d=256, 8 experts, 8 heads, 4 blocks, 4-layer MLPs and one
+input function of 805 points, fp32 arithmetic (the reference computes in fp32; the MoE GEMMs run on
+bf16 MFMA with an exact three-piece split, fp32-level results).  A step = pack weights -> GNOT forward
+(gnot_amd, HIP) -> RelL2 loss (loss.py:14-23) -> backward to every parameter gradient -> (N>1: one
+RCCL all-reduce of the flat gradient buffer) -> AdamW step.
+At N>1 ranks the default run point-shards ONE mesh of N x 262,144 points (weak scaling: 262,144 points
+per GPU; at 4 GPUs this is configs[3]'s 1,048,576-point mesh): every attention call all-reduces its
+states and runs the scramble all-to-all over RCCL.  Other workloads
+(--workload): cfg1 = configs[0] (main.py widths, batch 4 x 4096), cfg2 = configs[1] (d=128, 4 experts,
+2 input functions, 10k points), cfg4 = configs[3] as strong scaling (ONE 1,048,576-point mesh split
+over the ranks), cfg5 = configs[4] (64 variable meshes, LPT sample-DP).  --points / --meshes resize.
 
 value = all query points processed by all ranks / max-over-ranks wall time of the K timed steps.
-roofline: the dominant kernel (fused MoE expert chains, backward) timed live with hipEvents on
-its own stream during the timed steps; achieved = its algorithmic MFMA FLOPs / device time vs the
-fp32 MFMA peak (157.3 TFLOP/s, MI355X_MICROARCH.md).
-cpu_baseline: the stock-torch CPU port of the reference (oracle/torch_port.py) on this host's
-cores, same workload, rank 0 at N=1 only.
+roofline: the kernel class with the most device time in an untimed profiled step (normally the
+weight-gradient GEMMs or the MoE chain backward), timed live with hipEvents on the stream it runs on
+during the timed steps; achieved = its algorithmic FLOPs per launch / average launch duration vs the
+fp32 MFMA peak (157.3 TFLOP/s, MI355X_MICROARCH.md; the arithmetic is fp32).
+cpu_baseline: the stock-torch CPU port of the reference (oracle/torch_port.py) on this host's cores, on
+a bounded sample of the same model (one mesh of at most 16,384 points), rank 0 at N=1 only.
 """
 import argparse
 import json
@@ -58,28 +61,28 @@ WORKLOADS = {
                             n_input_hidden_dim=128, n_expert=4, n_head=8, n_input_functions=2),
                  N=10000, M=805, B=1,
                  desc="configs[1]: GNOT 4-layer, 4-expert, d=128, 8 heads, 2 input functions, "
-                      "2-D irregular mesh 10k points/sample (805 points per input function), fp32 fwd+bwd"),
+                      "2-D irregular mesh of {N} points/sample (805 points per input function), fp32 fwd+bwd"),
     # BASELINE.json configs[2]: synthetic 3-D mesh, 256k points, d=256, 8 experts (the reference
     # config is bf16; this path computes the reference's fp32)
     "cfg3": dict(model=dict(input_dim=3, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=4,
                             n_attn_hidden_dim=256, n_mlp_num_layers=4, n_mlp_hidden_dim=256,
                             n_input_hidden_dim=256, n_expert=8, n_head=8, n_input_functions=1),
-                 N=262144, M=805, B=1,
-                 desc="configs[2]: synthetic 3-D mesh 262,144 points/sample, d=256, 8 experts, 8 heads, "
+                 N=262144, M=805, B=1, shard_weak=True,
+                 desc="configs[2]: synthetic 3-D mesh of {N} points, d=256, 8 experts, 8 heads, "
                       "1 input function (805 points), fp32 fwd+bwd"),
     # BASELINE.json configs[3]: ONE 1M-point mesh point-sharded over the ranks (strong scaling)
     "cfg4": dict(model=dict(input_dim=3, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=4,
                             n_attn_hidden_dim=256, n_mlp_num_layers=4, n_mlp_hidden_dim=256,
                             n_input_hidden_dim=256, n_expert=8, n_head=8, n_input_functions=1),
                  N=1048576, M=805, B=1, shard=True,
-                 desc="configs[3]: synthetic 3-D mesh of 1,048,576 points point-sharded over the GPUs "
+                 desc="configs[3]: synthetic 3-D mesh of {N} points point-sharded over the GPUs "
                       "(state all-reduce + scramble all-to-all over RCCL), d=256, 8 experts, fp32 fwd+bwd"),
     # BASELINE.json configs[4]: 64 variable meshes (1k-50k points, packed), sample-DP with LPT balancing
     "cfg5": dict(model=dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=4,
                             n_attn_hidden_dim=256, n_mlp_num_layers=4, n_mlp_hidden_dim=256,
                             n_input_hidden_dim=256, n_expert=3, n_head=8, n_input_functions=1),
                  N=0, M=805, B=64, variable=(1000, 50000),
-                 desc="configs[4]: 64 meshes of U{1k..50k} points (seeded), packed offsets, sample-DP over the "
+                 desc="configs[4]: {B} meshes of U{{1k..50k}} points (seeded), packed offsets, sample-DP over the "
                       "GPUs with longest-processing-time balancing, main.py widths, fp32 fwd+bwd"),
     # BASELINE.json configs[0] (main.py defaults, ~1-4k points/sample, batch 4)
     "cfg1": dict(model=dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=4,
@@ -87,7 +90,7 @@ WORKLOADS = {
                             n_input_hidden_dim=256, n_expert=3, n_head=8, n_input_functions=1),
                  N=4096, M=805, B=4,
                  desc="configs[0]: main.py defaults d=256, 3 experts, 8 heads, 1 input function, "
-                      "batch 4 x 4096 points, fp32 fwd+bwd"),
+                      "batch {B} x {N} points, fp32 fwd+bwd"),
 }
 
 
@@ -128,16 +131,19 @@ def make_rank_batch(w, rank, world, device):
         to = lambda t: t.to(device)
         return dict(x=to(torch.cat(xs)), x_off=x_off, theta=to(torch.cat(th)), fns=[to(f) for f in fns],
                     fn_offs=fn_offs, y=to(torch.cat(ys)), seg=to(seg), B=Bl, norm=w["B"], n_global=None,
-                    step_points=sum(sizes))
-    if w.get("shard"):
+                    step_points=sum(sizes), mesh_points=f"{min(sizes)}..{max(sizes)}", meshes=w["B"])
+    if w.get("shard") or (w.get("shard_weak") and world > 1):
+        w = dict(w, N=w["N"] * (world if w.get("shard_weak") else 1))     # weak: N points per rank
         x, x_off, theta, fns, fn_offs, y, seg = make_batch(w, 100, torch.device("cpu"))
         lo, hi = par.shard_range(w["N"], rank, world)
         to = lambda t: t.to(device)
         return dict(x=to(x[lo:hi]), x_off=[0, hi - lo], theta=to(theta), fns=[to(f) for f in fns], fn_offs=fn_offs,
-                    y=to(y[lo:hi]), seg=to(seg[lo:hi]), B=1, norm=1, n_global=[w["N"]], step_points=w["N"])
+                    y=to(y[lo:hi]), seg=to(seg[lo:hi]), B=1, norm=1, n_global=[w["N"]], step_points=w["N"],
+                    mesh_points=f"{w['N']:,} ({hi - lo:,} on this GPU)", meshes=1)
     x, x_off, theta, fns, fn_offs, y, seg = make_batch(w, 100 + rank, device)
     return dict(x=x, x_off=x_off, theta=theta, fns=fns, fn_offs=fn_offs, y=y, seg=seg, B=w["B"],
-                norm=w["B"] * world, n_global=None, step_points=w["B"] * w["N"] * world)
+                norm=w["B"] * world, n_global=None, step_points=w["B"] * w["N"] * world, mesh_points=f"{w['N']:,}",
+                meshes=w["B"])
 
 
 def make_batch(w, seed, device):
@@ -155,8 +161,13 @@ def make_batch(w, seed, device):
     return to(x), x_off, to(theta), [to(f) for f in fns], fn_offs, to(y), to(seg)
 
 
-def cpu_baseline(w, steps=5, warmup=2):
-    """Reference CPU path (stock torch, oracle/torch_port.py) on this host's cores."""
+CPU_SAMPLE_POINTS = 16384      # bound on the CPU sample (points per step; ~10-30 s of host work)
+
+
+def cpu_baseline(w, steps=3, warmup=1):
+    """Reference CPU path (stock torch, oracle/torch_port.py) on this host's cores, on a BOUNDED sample
+    of the workload: the same model, one step over at most CPU_SAMPLE_POINTS query points (pts/s of
+    this linear-attention model is flat in the mesh size)."""
     from oracle import torch_port
     from gnot_amd import GNOT
     m = w["model"]
@@ -166,8 +177,12 @@ def cpu_baseline(w, steps=5, warmup=2):
                                 "n_input_hidden_dim", "n_expert", "n_head", "n_input_functions")])
     p = {k: v.detach().clone().requires_grad_(True) for k, v in mod.state_dict().items()}
     cfg = dict(m, d=m["n_attn_hidden_dim"])
-    x, x_off, theta, fns, fn_offs, y, seg = make_batch(w, 0, torch.device("cpu"))
-    B, N, M = w["B"], w["N"], w["M"]
+    B = max(1, min(w["B"], 4))
+    N = w["N"] if w["N"] > 0 else 4096
+    N = min(N, CPU_SAMPLE_POINTS // B)
+    ws = dict(w, B=B, N=N)
+    x, x_off, theta, fns, fn_offs, y, seg = make_batch(ws, 0, torch.device("cpu"))
+    M = w["M"]
     xb = x.view(B, N, -1)
     fb = [f.view(B, M, -1) for f in fns]
     times = []
@@ -182,9 +197,10 @@ def cpu_baseline(w, steps=5, warmup=2):
             times.append(time.perf_counter() - t0)
     med = statistics.median(times)
     return dict(value=round(B * N / med, 1), unit="points/s", cores=torch.get_num_threads(), kind="port",
-                sample=f"same workload ({B}x{N} points), stock-torch fp32 CPU port of the reference "
-                       f"(oracle/torch_port.py, fixture-validated), fwd+RelL2+bwd, median of {steps} "
-                       f"steps after {warmup} warm-up, {torch.get_num_threads()} threads")
+                sample=f"bounded sample of the workload: same model, {B} mesh(es) x {N} points ({M} input-function "
+                       f"points), stock-torch fp32 CPU port of the reference (oracle/torch_port.py, fixture-"
+                       f"validated), fwd+RelL2+bwd, median of {steps} steps after {warmup} warm-up, "
+                       f"{torch.get_num_threads()} threads; points/s is flat in the mesh size (linear attention)")
 
 
 def main():
@@ -192,10 +208,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", default="cfg2", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="cfg3", choices=sorted(WORKLOADS))
     ap.add_argument("--points", type=int, default=0, help="override points per sample")
     ap.add_argument("--meshes", type=int, default=0, help="cfg5: override the number of meshes")
-    ap.add_argument("--roofline-kernel", default="moe_bwd", choices=["moe_fwd", "moe_bwd", "wgrad"])
+    ap.add_argument("--roofline-kernel", default="auto", choices=["auto", "moe_fwd", "moe_bwd", "wgrad"],
+                    help="kernel class timed live for the roofline (auto: the one with the most device time)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--torch-adamw", action="store_true", help="torch's fused AdamW instead of the native one")
@@ -232,7 +249,7 @@ def main():
     model = GNOT(*[m[k] for k in ("input_dim", "theta_dim", "input_func_dim", "out_dim", "n_attn_layers",
                                   "n_attn_hidden_dim", "n_mlp_num_layers", "n_mlp_hidden_dim",
                                   "n_input_hidden_dim", "n_expert", "n_head", "n_input_functions")]).to(device)
-    shard = bool(w.get("shard")) and world > 1
+    shard = bool(w.get("shard") or w.get("shard_weak")) and world > 1
     # the point-shard exchanges run inside the engine's launch sequence (RCCL through callbacks): eager
     use_graph = not args.no_graph and not shard
     from gnot_amd import train as gtrain
@@ -292,25 +309,31 @@ def main():
             eager_step()
     torch.cuda.current_stream(device).wait_stream(side)
     torch.cuda.synchronize()
-    if args.breakdown:
-        for kind in ("moe_fwd", "moe_bwd", "wgrad"):
-            eng.profile_enable(kind)
-            eager_step()
-            ms, n, fl = eng.profile_read()
+    # which kernel class dominates device time: one profiled eager step per class (untimed)
+    kinds = {}
+    for kind in ("moe_fwd", "moe_bwd", "wgrad"):
+        eng.profile_enable(kind)
+        eager_step()
+        kinds[kind] = eng.profile_read()
+        if args.breakdown:
+            ms, n, fl = kinds[kind]
             print(f"[breakdown] {kind}: {ms:.3f} ms/step over {n} launches, "
                   f"{fl / ms / 1e9 if ms else 0:.1f} TFLOP/s", file=sys.stderr)
-        eng.profile_enable("")
-        torch.cuda.synchronize()
+    eng.profile_enable("")
+    torch.cuda.synchronize()
+    rkind = args.roofline_kernel
+    if rkind == "auto":
+        rkind = max(kinds, key=lambda k: kinds[k][0])
 
     step = eager_step
     if use_graph:
         # the roofline kernel's hipEvent pairs are recorded inside the captured graph, so the timed
         # replays carry them (the pool of events exists from one eager profiled step)
-        eng.profile_enable(args.roofline_kernel)
+        eng.profile_enable(rkind)
         eager_step()
         eng.profile_read()
         torch.cuda.synchronize()
-        eng.profile_enable(args.roofline_kernel)
+        eng.profile_enable(rkind)
         g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         with torch.cuda.graph(g_fb):
             fwd_bwd()
@@ -329,7 +352,7 @@ def main():
             step()
         torch.cuda.synchronize()
     else:
-        eng.profile_enable(args.roofline_kernel)
+        eng.profile_enable(rkind)
 
     if world > 1:
         dist.barrier()
@@ -361,12 +384,13 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "strong" if w.get("shard") else "weak",
+        "scaling": "strong" if (w.get("shard") and world > 1) else "weak",
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic: coords/theta/input-function rows U[0,1], targets N(0,1), seeded per rank; "
                 "random-init weights (torch.manual_seed)",
-        "config": {"workload": w["desc"], "points_per_step": D["step_points"], "samples_per_gpu": B,
+        "config": {"workload": w["desc"].format(N=D["mesh_points"], B=D["meshes"]),
+                   "points_per_step": D["step_points"], "samples_per_gpu": B,
                    "input_function_points": w["M"], "hidden": m["n_attn_hidden_dim"], "experts": m["n_expert"],
                    "heads": m["n_head"], "blocks": m["n_attn_layers"], "mlp_layers": m["n_mlp_num_layers"],
                    "input_functions": m["n_input_functions"],
@@ -375,19 +399,21 @@ def main():
         "roofline": {
             "kernel": {"moe_fwd": "chain_fwd_kernel (fused MoE expert chains, forward)",
                        "moe_bwd": "chain_bwd_kernel (fused MoE expert chains, backward)",
-                       "wgrad": "pgemm_kernel+pgemm_reduce_kernel (weight gradients)"}[args.roofline_kernel],
+                       "wgrad": "pgemm_x6_kernel+pgemm_reduce_kernel (weight gradients, bf16x6 MFMA)"}[rkind],
+            "class": rkind,
+            "class_ms_per_step": {k: round(v[0], 3) for k, v in kinds.items()},
             "bound": "mfma",
             "achieved": round(achieved, 3),
             "peak": FP32_MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s",
             "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
-            "traffic": None if args.points else pmc_traffic(args.workload, args.roofline_kernel),
+            "traffic": None if args.points else pmc_traffic(args.workload, rkind),
             "avg_launch_us": round(avg_launch_ms * 1e3, 2),
             "flops_per_launch": kflops / max(klaunch, 1),
             "launches": klaunch,
         },
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload in ("cfg1", "cfg2"):
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(w)
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -1,6 +1,6 @@
 // Kernel microbenchmark (diagnostics, not part of libgnot_hip.so): times the internal launchers on
 // synthetic cfg2-sized operands with hipEvents, one kernel class at a time, no contention.
-//   make microbench && ./microbench [points] [D]
+//   make microbench && ./microbench [points] [D] [experts]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -49,7 +49,7 @@ static double time_us(F&& f, int reps = 50) {
 int main(int argc, char** argv) {
   const int P = argc > 1 ? std::atoi(argv[1]) : 10000;
   const int D = argc > 2 ? std::atoi(argv[2]) : 128;
-  const int E = 4, NL = 5, DT = D / 16;
+  const int E = argc > 3 ? std::atoi(argv[3]) : 4, NL = 5, DT = D / 16;
   // packed weight images: NL layers x E chains, fwd and transposed (values arbitrary, finite)
   const size_t img4 = (size_t)DT * ((DT + 1) / 2) * 3 * 64;   // float4 per DxD image (bf16x6 >= fp32)
   float4* W = reinterpret_cast<float4*>(dalloc(img4 * 4 * NL * E * 2, 0.05f));
@@ -67,14 +67,14 @@ int main(int argc, char** argv) {
   float* Y = dalloc((size_t)E * P * D, 0.0f);
   float* save = dalloc((size_t)E * NL * P * D, 1.0f);
   float* dz = dalloc((size_t)E * NL * P * D, 0.0f);
-  float* scores = dalloc((size_t)P * 4, 0.25f);
-  float* dscore = dalloc((size_t)P * 4, 0.0f);
+  float* scores = dalloc((size_t)P * 16, 0.25f);
+  float* dscore = dalloc((size_t)P * 16, 0.0f);
   float* dX = dalloc((size_t)E * P * D, 0.0f);
 
   ChainArgs a{};
   a.D = D; a.KT0 = DT; a.OTL = DT; a.nlin = NL; a.in_dim = D; a.out_dim = D; a.P = P; a.nchains = E;
   a.layers = dlayers; a.X = X; a.ldx = D; a.Y = Y; a.ldy = D; a.y_chain_stride = (long)P * D;
-  a.scores = scores; a.ldsc = 4; a.mode = CH_MOE;
+  a.scores = scores; a.ldsc = 16; a.mode = CH_MOE;
   a.save = save; a.save_layer_stride = (long)P * D; a.save_chain_stride = (long)NL * P * D;
   const double fl = 2.0 * E * P * NL * (double)D * D;
   double t = time_us([&] { CK(launch_chain_fwd(a, nullptr)); });

@@ -73,6 +73,9 @@ class Engine:
         if geom == self.geom:
             return
         B = len(x_off) - 1
+        if self.comm is None and n_global is not None:
+            raise ValueError("n_global was given but no point-shard communicator is set "
+                             "(GNOT.set_point_shard): the local slice would be run as a whole mesh")
         if self.comm is not None:
             if n_global is None or len(n_global) != B:
                 raise ValueError("point-sharded GNOT needs n_global (global points of every sample)")
@@ -138,7 +141,8 @@ class Engine:
 
     # ---------------------------------------------------------------- compute
     def stream(self):
-        return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        """torch's current stream ON THE WORKSPACE'S DEVICE (not the current device's)."""
+        return ctypes.c_void_p(torch.cuda.current_stream(self.ws.device).cuda_stream)
 
     def forward(self, x, theta, fns, out):
         s = self.stream()
@@ -149,7 +153,8 @@ class Engine:
         return self.fwd_token
 
     def backward(self, dout):
-        _lib.check(self.lib.gnot_backward(self.plan, dout.data_ptr(), self.stream()))
+        with torch.cuda.device(self.ws.device):
+            _lib.check(self.lib.gnot_backward(self.plan, dout.data_ptr(), self.stream()))
         if self.grad_hook is not None:
             self.grad_hook(self.grad_arena)     # e.g. ONE all-reduce of all gradients (sample-DP)
         return self.grad_views

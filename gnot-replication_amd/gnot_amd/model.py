@@ -135,6 +135,7 @@ class GNOT(nn.Module):
                          n_input_hidden_dim=n_input_hidden_dim, n_expert=n_expert, n_head=n_head,
                          n_input_functions=n_input_functions)
         self._engine = None
+        self._comm = None          # parallel.PointShardComm (set_point_shard); survives engine rebuilds
 
     # canonical Linear order == named_parameters() order of the reference module
     def linears(self):
@@ -148,6 +149,7 @@ class GNOT(nn.Module):
     def engine(self):
         if self._engine is None:
             self._engine = Engine(self._cfg, self.linears())
+            self._engine.comm = self._comm
         return self._engine
 
     def _apply(self, fn, *args, **kwargs):
@@ -176,6 +178,7 @@ class GNOT(nn.Module):
     def set_point_shard(self, comm):
         """Shard every sample's points over the ranks of `comm` (gnot_amd.parallel.PointShardComm), or
         None to switch sharding off.  forward_packed then takes this rank's slices plus n_global."""
+        self._comm = comm
         self.engine().comm = comm
         self.engine().geom = None
 
@@ -193,6 +196,8 @@ class GNOT(nn.Module):
         params = [l.weight for l in self.linears()] + [l.bias for l in self.linears()]
         training = torch.is_grad_enabled() and any(p.requires_grad for p in params)
         eng = self.engine()
-        eng.prepare([int(v) for v in x_off], [[int(v) for v in o] for o in fn_offs], training, x.device,
-                    n_global=None if n_global is None else [int(n) for n in n_global])
-        return _GNOTFunction.apply(eng, x, theta, fns, self._cfg["out_dim"], *params)
+        # every launch (and the plan's side streams) on x's device, whatever device is current
+        with torch.cuda.device(x.device):
+            eng.prepare([int(v) for v in x_off], [[int(v) for v in o] for o in fn_offs], training, x.device,
+                        n_global=None if n_global is None else [int(n) for n in n_global])
+            return _GNOTFunction.apply(eng, x, theta, fns, self._cfg["out_dim"], *params)

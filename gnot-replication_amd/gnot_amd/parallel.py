@@ -13,6 +13,7 @@ Two modes, both with ONE gradient all-reduce of the flat gradient buffer per ste
 The reference itself is single-device (main.py:27); nothing here has a reference counterpart beyond
 the arithmetic it must reproduce.
 """
+import contextlib
 import ctypes
 import heapq
 import traceback
@@ -72,9 +73,11 @@ class PointShardComm:
     """gnot_comm backed by a torch.distributed process group.
 
     The engine hands over raw pointers into its workspace; they are wrapped as float32 views of the
-    workspace tensor (no copies).  With RCCL (`nccl` backend) the collectives are ordered on the
-    current HIP stream by torch.  `stage_via_host` routes them through host tensors instead (for the
-    gloo backend, e.g. several ranks sharing one GPU in tests)."""
+    workspace tensor (no copies).  With RCCL (`nccl` backend) every collective is issued on the
+    stream the engine passes (the one its kernels run on, wrapped as a torch ExternalStream), so it is
+    ordered after the producing kernels and before the consumers whatever torch's current stream is.
+    `stage_via_host` routes them through host tensors instead (for the gloo backend, e.g. several
+    ranks sharing one GPU in tests); the host copies then synchronise on that same stream."""
 
     def __init__(self, group=None, stage_via_host=False):
         self.group = group
@@ -92,16 +95,23 @@ class PointShardComm:
             raise RuntimeError("gnot_comm buffer outside the engine workspace")
         return self.ws[off: off + 4 * n].view(torch.float32)
 
+    def _on(self, stream):
+        """torch stream context for the engine's HIP stream handle (no-op for host buffers)."""
+        if self.ws is None or not self.ws.is_cuda:
+            return contextlib.nullcontext()
+        return torch.cuda.stream(torch.cuda.ExternalStream(int(stream or 0), device=self.ws.device))
+
     def _allreduce(self, user, buf, count, stream):
         try:
             if count > 0:
                 t = self._view(buf, count)
-                if self.stage:
-                    h = t.cpu()
-                    dist.all_reduce(h, group=self.group)
-                    t.copy_(h)
-                else:
-                    dist.all_reduce(t, group=self.group)
+                with self._on(stream):
+                    if self.stage:
+                        h = t.cpu()
+                        dist.all_reduce(h, group=self.group)
+                        t.copy_(h)
+                    else:
+                        dist.all_reduce(t, group=self.group)
             return 0
         except Exception:
             traceback.print_exc()
@@ -112,14 +122,15 @@ class PointShardComm:
             sc = [int(send_counts[i]) for i in range(self.world)]
             rc = [int(recv_counts[i]) for i in range(self.world)]
             dev = self.ws.device
-            s = self._view(send, sum(sc)) if sum(sc) else torch.empty(0, device=dev)
-            r = self._view(recv, sum(rc)) if sum(rc) else torch.empty(0, device=dev)
-            if self.stage:
-                hr = torch.empty(sum(rc), dtype=torch.float32)
-                dist.all_to_all_single(hr, s.cpu(), rc, sc, group=self.group)
-                r.copy_(hr)
-            else:
-                dist.all_to_all_single(r, s, rc, sc, group=self.group)
+            with self._on(stream):
+                s = self._view(send, sum(sc)) if sum(sc) else torch.empty(0, device=dev)
+                r = self._view(recv, sum(rc)) if sum(rc) else torch.empty(0, device=dev)
+                if self.stage:
+                    hr = torch.empty(sum(rc), dtype=torch.float32)
+                    dist.all_to_all_single(hr, s.cpu(), rc, sc, group=self.group)
+                    r.copy_(hr)
+                else:
+                    dist.all_to_all_single(r, s, rc, sc, group=self.group)
             return 0
         except Exception:
             traceback.print_exc()

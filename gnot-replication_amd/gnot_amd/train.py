@@ -185,53 +185,77 @@ def _to(batch, dev):
             batch["fn_offs"], batch["y"].to(dev))
 
 
+def _forward_batch(model, batch, dev):
+    """(prediction [sum N, out], packed offsets, target) of one batch.  Packed batches (collate_packed)
+    go through forward_packed; padded batches (collate_padded) through the reference calling
+    convention `model(x, theta, input_functions)` (main.py:84) and are un-padded with the real point
+    counts (main.py:87-89) -- the pad rows still enter the attention sums, exactly as in main.py."""
+    if "counts" in batch:
+        x = batch["x"].to(dev)
+        fns = batch["fns"].to(dev) if batch["fns"] is not None else None
+        out = model(x, batch["theta"].to(dev), fns)
+        counts = batch["counts"]
+        pred = torch.cat([out[b, :n] for b, n in enumerate(counts)])
+        off = [0]
+        for n in counts:
+            off.append(off[-1] + n)
+        return pred, off, batch["y"].to(dev)
+    x, x_off, theta, fns, fn_offs, y = _to(batch, dev)
+    return model.forward_packed(x, x_off, theta, fns, fn_offs), x_off, y
+
+
 def evaluate(model, loader, loss_fn=None):
-    """main.py:108-147: mean RelL2 over the test batches, no_grad (no activations kept)."""
+    """main.py:108-147: mean RelL2 over the test batches, no_grad (no activations kept).  Batches from
+    collate_padded reproduce main.py's padded evaluation; collate_packed batches the unpadded one."""
     loss_fn = loss_fn or RelL2Loss()
     dev = next(model.parameters()).device
     vals = []
     with torch.no_grad():
         for batch in loader:
-            x, x_off, theta, fns, fn_offs, y = _to(batch, dev)
-            out = model.forward_packed(x, x_off, theta, fns, fn_offs)
-            vals.append(float(loss_fn(x_off, out, y)))
+            pred, off, y = _forward_batch(model, batch, dev)
+            vals.append(float(loss_fn(off, pred, y)))
     return sum(vals) / max(len(vals), 1)
 
 
 def fit(model, train_loader, test_loader=None, epochs=100, lr=1e-3, per_epoch_schedule=True, checkpoint=None,
         log=print):
-    """The reference training loop (main.py:50-153) on packed batches: AdamW(lr) + OneCycleLR(max_lr=lr,
-    steps_per_epoch, epochs), RelL2 loss, per-epoch test metric and best checkpoint.  With
-    per_epoch_schedule=True the schedule is stepped once per epoch, as main.py:106 does.
+    """The reference training loop (main.py:50-153): AdamW(lr) + OneCycleLR(max_lr=lr, steps_per_epoch,
+    epochs), RelL2 loss, per-epoch test metric and best checkpoint.  With per_epoch_schedule=True the
+    schedule is stepped once per epoch, as main.py:106 does.  The loaders decide the batch form:
+    collate_padded batches run main.py's zero-padded semantics (pad rows in the attention sums),
+    collate_packed batches the packed (per-sample exact) one.
     Returns (train losses per epoch, test metrics per epoch)."""
-    dev = next(model.parameters()).device
     flat = flatten_parameters(model)
     sched = OneCycle(lr, epochs, len(train_loader))
     opt = FlatAdamW(flat, lr=lr, schedule=sched)
+    dev = flat.device
     eng = model.engine()
-    eng.param_grads = False
+    prev = eng.param_grads
+    eng.param_grads = False          # FlatAdamW reads the gradient arena; no .grad copies
     loss_fn = RelL2Loss()
     best, hist_train, hist_test = float("inf"), [], []
-    for epoch in range(epochs):
-        losses = []
-        for batch in train_loader:
-            x, x_off, theta, fns, fn_offs, y = _to(batch, dev)
-            out = model.forward_packed(x, x_off, theta, fns, fn_offs)
-            loss = loss_fn(x_off, out, y)
-            loss.backward()
-            opt.step(eng.grad_flat)
-            if not per_epoch_schedule:
+    try:
+        for epoch in range(epochs):
+            losses = []
+            for batch in train_loader:
+                pred, off, y = _forward_batch(model, batch, dev)
+                loss = loss_fn(off, pred, y)
+                loss.backward()
+                opt.step(eng.grad_flat)
+                if not per_epoch_schedule:
+                    sched.step()
+                losses.append(float(loss))
+            if per_epoch_schedule:
                 sched.step()
-            losses.append(float(loss))
-        if per_epoch_schedule:
-            sched.step()
-        hist_train.append(sum(losses) / max(len(losses), 1))
-        log(f"Epoch {epoch}, Loss: {hist_train[-1]}")
-        if test_loader is not None:
-            res = evaluate(model, test_loader, loss_fn)
-            hist_test.append(res)
-            log(f"Epoch {epoch}, Test Metric: {res}")
-            if res < best and checkpoint:
-                best = res
-                save_checkpoint(model, checkpoint)
+            hist_train.append(sum(losses) / max(len(losses), 1))
+            log(f"Epoch {epoch}, Loss: {hist_train[-1]}")
+            if test_loader is not None:
+                res = evaluate(model, test_loader, loss_fn)
+                hist_test.append(res)
+                log(f"Epoch {epoch}, Test Metric: {res}")
+                if res < best and checkpoint:
+                    best = res
+                    save_checkpoint(model, checkpoint)
+    finally:
+        eng.param_grads = prev       # ordinary autograd use after fit() gets .grad again
     return hist_train, hist_test

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Train GNOT on NS2d-format data with the MI355X core: the reference's main.py (argparse flags of
 main.py:15-23, batch 4, AdamW lr 1e-3, OneCycleLR stepped per epoch, RelL2 metric, best checkpoint)
-on packed batches instead of dgl graphs + padding.
+with plain tensors instead of dgl graphs.  Batches are zero-padded exactly like main.py:60-89 by
+default (the pad rows enter the attention sums, as in the reference); --packed uses packed offsets.
 
     python scripts/train_ns2d.py --train train.pkl --test test.pkl [--epochs 100 ...]
     python scripts/train_ns2d.py --synthetic 64 --epochs 2          # generated meshes, same format
@@ -36,6 +37,8 @@ def main():
     ap.add_argument("--batch", type=int, default=4)
     ap.add_argument("--per-batch-schedule", action="store_true", help="step OneCycleLR per batch (main.py steps it per epoch)")
     ap.add_argument("--checkpoint", default="best_model.pth")
+    ap.add_argument("--packed", action="store_true",
+                    help="packed batches (per-sample exact); default: main.py's zero-padded batches")
     args = ap.parse_args()
     if args.synthetic:
         rng = np.random.default_rng(0)
@@ -49,7 +52,8 @@ def main():
                  args.n_attn_hidden_dim, args.n_mlp_num_layers, args.n_mlp_hidden_dim, args.n_input_hidden_dim,
                  args.n_expert, args.n_head, len(f0)).to(dev)
     dl = lambda ds, sh: torch.utils.data.DataLoader(ds, batch_size=args.batch, shuffle=sh,
-                                                    collate_fn=data.collate_packed)
+                                                    collate_fn=data.collate_packed if args.packed
+                                                    else data.collate_padded)
     _, test = train.fit(model, dl(tr, True), dl(te, False), epochs=args.epochs,
                         per_epoch_schedule=not args.per_batch_schedule, checkpoint=args.checkpoint)
     print(f"\nBest Test Metric: {min(test)}")
