@@ -62,6 +62,7 @@ struct WgradGroup {
   int total_wgs = 0, total_red = 0;
   size_t slab_floats = 0;
   bool x6 = false;                   // plain weight-gradient jobs: the bf16x6 MFMA kernel
+  bool wide = false;                 // ... on the 256 x 256-tile kernel (d = 256: one workgroup per job split)
   int state_pts = 0, state_nw = 0;   // state groups: points per workgroup, per-point weights (0 or H)
   WgradJob* d_jobs = nullptr;        // device copies (workspace tables)
   int* d_wg_prefix = nullptr;
@@ -480,12 +481,18 @@ static void finish_group(gnot_plan* p, WgradGroup& G) {
   // the x6 kernel holds ~240 registers per lane: one workgroup per CU leaves the other half of
   // every SIMD's register file to the concurrent main-stream kernels (env GNOT_X6_WGS overrides)
   static const long x6_wgs = std::getenv("GNOT_X6_WGS") ? std::atol(std::getenv("GNOT_X6_WGS")) : 256;
-  const long target = G.x6 ? x6_wgs : kTargetWGs;
+  // d = 256: every job's whole 256 x 256 gradient in one workgroup (8 waves, 96 KiB LDS: one per CU)
+  static const bool no_wide = std::getenv("GNOT_NO_WIDE") != nullptr;
+  static const long wide_wgs = std::getenv("GNOT_WIDE_WGS") ? std::atol(std::getenv("GNOT_WIDE_WGS")) : 256;
+  G.wide = G.x6 && !no_wide && p->D == 256 && !G.jobs.empty();
+  for (const auto& J : G.jobs)
+    if (J.out > 256 || J.in > 256) G.wide = false;
+  const long target = G.wide ? wide_wgs : G.x6 ? x6_wgs : kTargetWGs;
   long tiles = 0;
   for (auto& J : G.jobs) {
     J.tiles_o = (J.out + kPTile - 1) / kPTile;
     J.tiles_i = (J.in + kPTile - 1) / kPTile;
-    tiles += J.diag_only ? J.tiles_o : J.tiles_o * J.tiles_i;
+    tiles += G.wide ? 1 : J.diag_only ? J.tiles_o : J.tiles_o * J.tiles_i;
   }
   // floor, not ceil: never more than `target` workgroups, so no CU runs one more than planned
   const long want = std::max<long>(1, target / std::max<long>(tiles, 1));
@@ -501,7 +508,7 @@ static void finish_group(gnot_plan* p, WgradGroup& G) {
     J.slab_off = (long)G.slab_floats;
     G.slab_floats += (size_t)J.splits * nt * kPTile * (kPTile + 1);
     G.wg_prefix.push_back(wg);
-    wg += nt * J.splits;
+    wg += (G.wide ? 1 : nt) * J.splits;
     G.red_prefix.push_back(red);
     red += nt * kPTile * (kPTile + 1);
   }
@@ -1343,7 +1350,7 @@ int run_wgrad_side(Ctx& c, const WgradGroup& G, std::initializer_list<const floa
     float* slab = c.s == p->side2 ? p->P_("slab_wgrad2") : p->P_("slab_wgrad");
     ProfScope ps(c, "wgrad", group_flops(G));
     GNOT_CK(launch_wgrad(G.d_jobs, G.d_wg_prefix, (int)G.jobs.size(), G.total_wgs, G.d_red_prefix,
-                         G.total_red, slab, c.s, G.x6));
+                         G.total_red, slab, c.s, G.x6, G.wide));
     return GNOT_OK;
   }
   hipEvent_t fork = next_event(p);
@@ -1352,7 +1359,7 @@ int run_wgrad_side(Ctx& c, const WgradGroup& G, std::initializer_list<const floa
   {
     ProfScope ps(c, "wgrad", group_flops(G), p->side);
     GNOT_CK(launch_wgrad(G.d_jobs, G.d_wg_prefix, (int)G.jobs.size(), G.total_wgs, G.d_red_prefix,
-                         G.total_red, p->P_("slab_wgrad"), p->side, G.x6));
+                         G.total_red, p->P_("slab_wgrad"), p->side, G.x6, G.wide));
   }
   hipEvent_t done = next_event(p);
   GNOT_CK(hipEventRecord(done, p->side));

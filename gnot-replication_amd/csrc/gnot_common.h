@@ -292,6 +292,16 @@ constexpr int x6_chunk_f4(int KT, int OT) { return x6_och<D>(KT, OT) * x6_tch<D>
 GNOT_DEV unsigned f2u(float x) { return __builtin_bit_cast(unsigned, x); }
 GNOT_DEV float u2f(unsigned x) { return __builtin_bit_cast(float, x); }
 
+// ---- buffer loads: base + bound in SGPRs (reads past `bytes` return 0), wave-uniform row offset in
+// an SGPR (soffset), only the lane's column offset in a VGPR
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+GNOT_DEV rsrc_t make_rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+GNOT_DEV float buf_load_f32(rsrc_t r, int voff, int soff) {
+  return u2f(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+
 // exact 3-piece truncation split of 8 floats: p[q] = 8 bf16 (4 dwords, element j in the low half
 // of dword j/2 for even j) of piece q; v == piece0 + piece1 + piece2 exactly
 GNOT_DEV void split8_x6(const float (&v)[8], u32x4 (&p)[3]) {

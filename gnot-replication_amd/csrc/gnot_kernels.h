@@ -104,8 +104,11 @@ struct WgradJob {
 // one workgroup per (job, tile, split); wg_prefix / red_prefix: per-job prefix sums of workgroups and
 // of reduce elements (ntile * 128 * 129)
 // x6: plain weight-gradient jobs only (no w, state_dh, diag_only) on the bf16x6 MFMA kernel
+// wide: the same on the 256 x 256-tile kernel (out, in <= 256; ONE workgroup per (job, split), so
+//       wg_prefix counts splits only)
 hipError_t launch_wgrad(const WgradJob* jobs_dev, const int* wg_prefix_dev, int njobs, int total_wgs,
-                        const int* red_prefix_dev, int total_red, float* slab, hipStream_t s, bool x6 = false);
+                        const int* red_prefix_dev, int total_red, float* slab, hipStream_t s, bool x6 = false,
+                        bool wide = false);
 
 // ------------------------------------------------------------------ attention states (state.hip)
 // Jobs are WgradJobs with state_dh > 0: A = dz/lddz, B = x/ldx, optional w/ldw, out = dW as

@@ -145,6 +145,39 @@ int main(int argc, char** argv) {
     for (size_t i = 0; i < ndw; ++i) { num += (got[i] - ref[i]) * (double)(got[i] - ref[i]); den += (double)ref[i] * ref[i]; }
     std::printf("wgrad MoE  bf16x6:                     %8.2f us  %6.1f TFLOP/s  (rel-L2 vs fp32 %.2e)\n", t, fl / t / 1e6,
                 std::sqrt(num / (den + 1e-30)));
+    if (D == 256) {   // the 256 x 256-tile kernel: one workgroup per (job, split)
+      for (int wgs : {256, 512}) {
+        std::vector<WgradJob> wj(jobs);
+        std::vector<int> wpre;
+        long soff = 0;
+        const int splits = std::max(1, wgs / njobs);
+        for (int k = 0; k < njobs; ++k) {
+          wj[k].splits = splits;
+          wj[k].slab_off = soff;
+          soff += (long)splits * tiles * 128 * 129;
+          wpre.push_back(k * splits);
+        }
+        wpre.insert(wpre.end(), red_pre.begin(), red_pre.end());
+        WgradJob* dwj = nullptr;
+        int* dwpre = nullptr;
+        float* wslab = nullptr;
+        CK(hipMalloc(&dwj, wj.size() * sizeof(WgradJob)));
+        CK(hipMemcpy(dwj, wj.data(), wj.size() * sizeof(WgradJob), hipMemcpyHostToDevice));
+        CK(hipMalloc(&dwpre, wpre.size() * sizeof(int)));
+        CK(hipMemcpy(dwpre, wpre.data(), wpre.size() * sizeof(int), hipMemcpyHostToDevice));
+        CK(hipMalloc(&wslab, soff * sizeof(float)));
+        t = time_us([&] { CK(launch_wgrad(dwj, dwpre, njobs, njobs * splits, dwpre + njobs, red, wslab, nullptr, true, true)); }, 20);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(got.data(), dW, ndw * 4, hipMemcpyDeviceToHost));
+        double n2 = 0, d2 = 0;
+        for (size_t i = 0; i < ndw; ++i) { n2 += (got[i] - ref[i]) * (double)(got[i] - ref[i]); d2 += (double)ref[i] * ref[i]; }
+        std::printf("wgrad MoE  bf16x6 wide 256x256 (%d WGs):  %8.2f us  %6.1f TFLOP/s  (rel-L2 vs fp32 %.2e)\n",
+                    njobs * splits, t, fl / t / 1e6, std::sqrt(n2 / (d2 + 1e-30)));
+        CK(hipFree(dwj));
+        CK(hipFree(dwpre));
+        CK(hipFree(wslab));
+      }
+    }
     {
       std::vector<WgradJob> ng(jobs);
       for (auto& J : ng) J.x_gelu = 0;

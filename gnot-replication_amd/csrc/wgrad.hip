@@ -14,6 +14,9 @@
 // is consumed.  Each wave computes a 64x64 quadrant with v_mfma_f32_32x32x2_f32 (2 points per MFMA
 // k-step, 4 MFMAs per pair of A/B fragment loads).  Partial tiles go to a slab; the reduce pass sums
 // the splits in a fixed order (deterministic, no atomics).
+#include <cstdlib>
+#include <type_traits>
+
 #include "gnot_common.h"
 #include "gnot_kernels.h"
 
@@ -345,6 +348,220 @@ __global__ void __launch_bounds__(256) pgemm_x6_kernel(const WgradJob* __restric
   }
 }
 
+// ---------------------------------------------------------------- wide bf16x6 variant (d = 256 weight gradients)
+// One workgroup owns a job's WHOLE 256 x 256 output (out, in <= 256) for one split-K point range, so
+// every staged dZ / X value is loaded, GELU'd and split exactly once (the 128 x 128 kernel above
+// stages each value twice and splits it on the same wave that issues the MFMAs).  8 waves, two per
+// SIMD (<= 256 registers each: the accumulators are 8 32x32 blocks = 128 AGPRs), so one wave's
+// staging VALU runs beside its partner's MFMAs.
+//   staging: thread t owns feature f = t & 255 and point half h = t >> 8 of a 16-point stage, for both
+//            operands: 8 dword loads per operand (a wave-instruction reads 256 contiguous bytes of one
+//            row), then 3 bf16 pieces of 8 consecutive points = three 16-byte LDS stores.
+//   LDS:     per (buffer, operand, piece) a fragment-order image of 8 row blocks x 64 lanes x 16 B:
+//            lane (r, h) of block rb holds rows 32 rb + r, points 8h .. 8h+7 -- the A/B operand layout of
+//            v_mfma_f32_32x32x16_bf16, so fragment reads are contiguous 1 KiB ds_read_b128.
+//   MFMA:    wave (wr, wc) computes rows [128 wr, +128) x cols [64 wc, +64): 4 x 2 blocks, six order <= 2
+//            piece products each (smallest first), one accumulator per block.
+// Double-buffered: stage s+1 is split into the other buffer while stage s is multiplied; its rows were
+// loaded one stage earlier.  Partials go to the same slab layout as pgemm_kernel (128-tiles).
+constexpr int kWStage = 16;
+constexpr int kWThreads = 512;
+constexpr int kWPiece = 8 * 64;                  // u32x4 per (operand, piece) image
+constexpr int kWBuf = 6 * kWPiece;               // A pieces 0..2 | B pieces 0..2
+constexpr size_t kWLdsBytes = 2 * kWBuf * 16;    // 96 KiB
+
+GNOT_DEV void x6_mfma6(const u32x4 (&a)[3], const u32x4 (&b)[3], f32x16& c) {
+#define GNOT_MFMA32(X, Y) \
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, X), __builtin_bit_cast(bf16x8, Y), c, 0, 0, 0)
+  GNOT_MFMA32(a[2], b[0]);
+  GNOT_MFMA32(a[1], b[1]);
+  GNOT_MFMA32(a[0], b[2]);
+  GNOT_MFMA32(a[1], b[0]);
+  GNOT_MFMA32(a[0], b[1]);
+  GNOT_MFMA32(a[0], b[0]);
+#undef GNOT_MFMA32
+}
+
+template <int V>
+__global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __restrict__ jobs,
+                                                              const int* __restrict__ prefix, int njobs,
+                                                              float* __restrict__ slab) {
+  extern __shared__ __attribute__((aligned(16))) u32x4 wl[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int j = find_job(prefix, njobs, blockIdx.x);
+  const WgradJob J = jobs[j];
+  const int split = blockIdx.x - prefix[j];
+  const int chunk = ((J.P + J.splits - 1) / J.splits + kWStage - 1) / kWStage * kWStage;
+  const long pb = (long)split * chunk;
+  const long pe = min((long)J.P, pb + chunk);
+  // staging role (the point half hh is wave-uniform: waves 0-3 / 4-7)
+  const int f = tid & 255, hh = tid >> 8;
+  const bool fa = f < J.out, fb = f < J.in;
+  const int fca = min(f, J.out - 1), fcb = min(f, J.in - 1);
+  const int sdst = (f >> 5) * 64 + (f & 31) + 32 * hh;
+  // MFMA role
+  const int wr = wave >> 2, wc = wave & 3;
+  const int nrb = max(0, min(4, (J.out - 128 * wr + 31) / 32));
+  const int ncb = max(0, min(2, (J.in - 64 * wc + 31) / 32));
+  const bool full = nrb == 4 && ncb == 2;
+  const bool gel = J.x_gelu != 0;
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{};
+  float dbacc = 0.f;
+  struct Raw {
+    float a[8], b[8];
+  };
+  // buffer loads: rows past the job's P read 0 (only the last split ends inside a stage: chunks are
+  // whole stages), columns past out / in are masked; the row offset is wave-uniform (SGPR)
+  const rsrc_t rA = make_rsrc(J.dz, (unsigned)min((long)J.P * J.lddz * 4, 0xFFFFFFFFL));
+  const rsrc_t rB = make_rsrc(J.x, (unsigned)min((long)J.P * J.ldx * 4, 0xFFFFFFFFL));
+  const int voA = fca * 4, voB = fcb * 4;
+  const int hw = __builtin_amdgcn_readfirstlane(hh);
+  auto load = [&](Raw& R, long p0) {
+    const unsigned pr = (unsigned)(p0 + 8 * hw);
+    // raw values only: any arithmetic on them here would make the wave wait for the load now
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      R.a[k] = buf_load_f32(rA, voA, (int)((pr + k) * (unsigned)J.lddz * 4u));
+      R.b[k] = buf_load_f32(rB, voB, (int)((pr + k) * (unsigned)J.ldx * 4u));
+    }
+  };
+  // split + LDS store of the staged rows; gel is uniform per workgroup: one branch around the whole
+  // stage (not per element), so each variant is one straight-line block the scheduler can interleave
+  auto stage_v = [&](int buf, const Raw& R, auto GEL) {
+    float ra[8], vb[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      ra[k] = fa ? R.a[k] : 0.f;                  // columns past out / in
+      const float b = fb ? R.b[k] : 0.f;
+      dbacc += ra[k];
+      vb[k] = decltype(GEL)::value ? gelu(b) : b;
+    }
+    u32x4 pa[3], pq[3];
+    split8_x6(ra, pa);
+    split8_x6(vb, pq);
+    u32x4* base = wl + buf * kWBuf;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      base[q * kWPiece + sdst] = pa[q];
+      base[(3 + q) * kWPiece + sdst] = pq[q];
+    }
+  };
+  auto stage = [&](int buf, const Raw& R) {
+    if (gel) stage_v(buf, R, std::true_type{});
+    else stage_v(buf, R, std::false_type{});
+  };
+  auto compute = [&](int buf) {
+    const u32x4* A = wl + buf * kWBuf;
+    const u32x4* Bm = A + 3 * kWPiece;
+    u32x4 bf[2][3];
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) bf[jb][q] = Bm[q * kWPiece + (wc * 2 + jb) * 64 + lane];
+    if (full) {
+      // row-block fragments one block ahead (two sets live: the register budget of two waves per SIMD)
+      u32x4 af[2][3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) af[0][q] = A[q * kWPiece + (wr * 4) * 64 + lane];
+#pragma unroll
+      for (int ib = 0; ib < 4; ++ib) {
+        if (ib + 1 < 4) {
+#pragma unroll
+          for (int q = 0; q < 3; ++q) af[(ib + 1) & 1][q] = A[q * kWPiece + (wr * 4 + ib + 1) * 64 + lane];
+        }
+        x6_mfma6(af[ib & 1], bf[0], acc[ib][0]);
+        x6_mfma6(af[ib & 1], bf[1], acc[ib][1]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+#pragma unroll
+      for (int ib = 0; ib < 4; ++ib) {
+        if (ib >= nrb) break;
+        u32x4 af[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) af[q] = A[q * kWPiece + (wr * 4 + ib) * 64 + lane];
+        if (ncb > 0) x6_mfma6(af, bf[0], acc[ib][0]);
+        if (ncb > 1) x6_mfma6(af, bf[1], acc[ib][1]);
+      }
+    }
+  };
+
+  // V & 1: the first half of the waves (w and w + 4 share a SIMD) runs at raised issue priority, so
+  //        after a barrier it gets through its MFMAs first and stages while its partner multiplies
+  // V & 2: two raw register sets (the rows of stage s+2 in flight for two stages)
+  if ((V & 1) && wave < 4) __builtin_amdgcn_s_setprio(1);
+  if constexpr ((V & 2) == 0) {
+    Raw R;
+    if (pb < pe) {
+      load(R, pb);
+      stage(0, R);
+      if (pb + kWStage < pe) load(R, pb + kWStage);
+    }
+    __syncthreads();
+    int buf = 0;
+    for (long p0 = pb; p0 < pe; p0 += kWStage) {
+      compute(buf);
+      if (p0 + kWStage < pe) {
+        stage(buf ^ 1, R);
+        if (p0 + 2 * kWStage < pe) load(R, p0 + 2 * kWStage);
+      }
+      __syncthreads();
+      buf ^= 1;
+    }
+  } else {
+    Raw R0, R1;
+    if (pb < pe) {
+      load(R0, pb);
+      if (pb + kWStage < pe) load(R1, pb + kWStage);
+      stage(0, R0);
+      if (pb + 2 * kWStage < pe) load(R0, pb + 2 * kWStage);
+    }
+    __syncthreads();
+    auto body = [&](long p0, int buf, Raw& Rn) {        // Rn: raw rows of stage p0 + kWStage
+      compute(buf);
+      if (p0 + kWStage < pe) {
+        stage(buf ^ 1, Rn);
+        if (p0 + 3 * kWStage < pe) load(Rn, p0 + 3 * kWStage);
+      }
+      __syncthreads();
+    };
+    for (long p0 = pb; p0 < pe; p0 += 2 * kWStage) {
+      body(p0, 0, R1);
+      if (p0 + kWStage < pe) body(p0 + kWStage, 1, R0);
+    }
+  }
+
+  // partials -> slab [split][128-tile][128 x (128 + 1)] (the pgemm_kernel layout)
+  const int ntile = J.tiles_o * J.tiles_i;
+  float* S0 = slab + J.slab_off + (long)split * ntile * (kTile * (kTile + 1));
+#pragma unroll
+  for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wr * 128 + ib * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int col = wc * 64 + jb * 32 + (lane & 31);
+        if (row < J.out && col < J.in)
+          S0[((row >> 7) * J.tiles_i + (col >> 7)) * (kTile * (kTile + 1)) + (row & 127) * (kTile + 1) + (col & 127)] =
+              acc[ib][jb][r];
+      }
+  if (J.db != nullptr) {
+    // column sums of A: the two point halves of every feature through LDS, in a fixed order
+    float* red = reinterpret_cast<float*>(wl);
+    red[hh * 256 + f] = dbacc;
+    __syncthreads();
+    if (tid < 256 && f < J.out)
+      S0[((f >> 7) * J.tiles_i) * (kTile * (kTile + 1)) + (f & 127) * (kTile + 1) + kTile] = red[f] + red[256 + f];
+  }
+}
+
 // sum the split partials; normal jobs write dW[out, in] (+ db[out]); state jobs (state_dh > 0) write
 // the per-head diagonal blocks into [H][dh*dh + dh] (S row-major, then z)
 __global__ void __launch_bounds__(256) pgemm_reduce_kernel(const WgradJob* __restrict__ jobs,
@@ -394,9 +611,26 @@ __global__ void __launch_bounds__(256) pgemm_reduce_kernel(const WgradJob* __res
 }
 
 hipError_t launch_wgrad(const WgradJob* jobs_dev, const int* wg_prefix_dev, int njobs, int total_wgs,
-                        const int* red_prefix_dev, int total_red, float* slab, hipStream_t s, bool x6) {
+                        const int* red_prefix_dev, int total_red, float* slab, hipStream_t s, bool x6, bool wide) {
   if (njobs <= 0) return hipSuccess;
-  if (x6)
+  if (wide) {
+    // GNOT_X6W_VARIANT (diagnostics): bit 0 priority split, bit 1 two raw register sets
+    static const int var = std::getenv("GNOT_X6W_VARIANT") ? std::atoi(std::getenv("GNOT_X6W_VARIANT")) & 3 : 0;
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(pgemm_x6w_kernel<0>), hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWLdsBytes);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(pgemm_x6w_kernel<1>), hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWLdsBytes);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(pgemm_x6w_kernel<2>), hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWLdsBytes);
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(pgemm_x6w_kernel<3>), hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWLdsBytes);
+      attr = true;
+    }
+    switch (var) {
+#define GNOT_X6W(V_) \
+  case V_: hipLaunchKernelGGL(pgemm_x6w_kernel<V_>, dim3(total_wgs), dim3(kWThreads), kWLdsBytes, s, jobs_dev, wg_prefix_dev, njobs, slab); break;
+      GNOT_X6W(0) GNOT_X6W(1) GNOT_X6W(2) GNOT_X6W(3)
+#undef GNOT_X6W
+    }
+  } else if (x6)
     hipLaunchKernelGGL(pgemm_x6_kernel, dim3(total_wgs), dim3(256), 0, s, jobs_dev, wg_prefix_dev, njobs, slab);
   else
     hipLaunchKernelGGL(pgemm_kernel, dim3(total_wgs), dim3(256), 0, s, jobs_dev, wg_prefix_dev, njobs, slab);
