@@ -140,6 +140,11 @@ constexpr int lds_och(int KT, int OT) {
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
 typedef __attribute__((address_space(1))) const void* global_cvoid_ptr;
 
+// LDS-DMA (global_load_lds) writes are tracked ONLY by the issuing wave's vmcnt: a barrier alone does
+// not make them visible (the compiler's workgroup fence waits for stores, not loads).  Every barrier
+// that hands DMA'd LDS to other waves is preceded by this wait.
+GNOT_DEV void lds_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 // copy n4 float4 (a multiple of 64) from global to LDS; all threads of the workgroup call this
 GNOT_DEV void stage_image(float4* lds, const float4* __restrict__ g, int n4, int nwaves, int wave, int lane) {
   for (int base = wave * WAVE; base < n4; base += nwaves * WAVE)
@@ -156,7 +161,8 @@ GNOT_DEV void mm_tiles_lds(const float4* __restrict__ Wg, float4* lds, const flo
   for (int c = 0; c < OT / OCH; ++c) {
     __syncthreads();                                   // previous readers of lds are done
     stage_image(lds, Wg + c * OCH * KT * WAVE, OCH * KT * WAVE, nwaves, wave, lane);
-    __syncthreads();                                   // drains the LDS-DMA (vmcnt(0)) + barrier
+    lds_dma_wait();
+    __syncthreads();
     // fragments of k-tile T+1 are read from LDS while the MFMAs of k-tile T run; within a k-tile the
     // MFMA order is k-step-outer / output-tile-inner, so consecutive MFMAs use independent
     // accumulators (the f32 16x16x4 MFMA has a 40-cycle dependent latency vs 32-cycle issue)
@@ -189,7 +195,7 @@ GNOT_DEV void mm_tiles_lds(const float4* __restrict__ Wg, float4* lds, const flo
 // Two LDS buffers of kChunkKB each.  A layer's image is consumed in chunks of `och` output tiles; while
 // chunk i is multiplied, chunk i+1 (of this layer, or the first chunk of the NEXT layer) is already
 // landing in the other buffer by LDS-DMA, so the weight stream never stalls the MFMAs at a layer
-// boundary.  One barrier per chunk: it retires chunk i's DMA (the barrier's vmcnt(0)) and frees the
+// boundary.  One barrier per chunk (after an explicit vmcnt(0)): it retires chunk i's DMA and frees the
 // buffer chunk i-1 used.  `cnt` counts consumed chunks (buffer parity).
 constexpr int kChunkKB = 16;
 constexpr int kChunkF4 = kChunkKB * WAVE;          // float4 per buffer
@@ -214,6 +220,7 @@ GNOT_DEV void mm_tiles_pipe(const float4* __restrict__ Wg, const float4* __restr
   constexpr int CH4 = OCH * KT * WAVE;
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
+    lds_dma_wait();                                    // this chunk's DMA (issued one chunk ago) has landed
     __syncthreads();
     float4* nb = lds + ((cnt + 1) & 1) * kChunkF4;
     if (c + 1 < NC) stage_image(nb, Wg + (c + 1) * CH4, CH4, nwaves, wave, lane);
@@ -365,6 +372,7 @@ GNOT_DEV void mm_tiles_pipe_x6(const float4* __restrict__ Wg, const float4* __re
 #pragma unroll
     for (int og = 0; og < NOG; ++og) {
       const int c = tg * NOG + og;
+      lds_dma_wait();
       __syncthreads();
       float4* nb = lds + ((cnt + 1) & 1) * kBufF4;
       if (c + 1 < NTG * NOG) stage_image(nb, Wg + (c + 1) * CH4, CH4, nwaves, wave, lane);

@@ -68,7 +68,8 @@ __global__ void __launch_bounds__(kStateThreads) state_partial_kernel(const Wgra
     if (use_w)
       for (int f = tid; f < np * H; f += kStateThreads) Ws[f] = J.w[(p0 + f / H) * J.ldw + f % H];
   }
-  __syncthreads();   // drains the LDS-DMA (vmcnt(0)) + barrier
+  lds_dma_wait();
+  __syncthreads();
   const int R = nblk >= kStateThreads ? 1 : kStateThreads / nblk;
   const int r = tid / (nblk < kStateThreads ? nblk : kStateThreads);
   float keep[20];
