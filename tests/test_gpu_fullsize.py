@@ -53,4 +53,6 @@ def test_configs2_full_size_properties():
     out = model.forward_packed(x, x_off, theta, fns, fn_offs)
     losses.append(loss_fn(x_off, out, y).item())
     assert all(torch.isfinite(torch.tensor(losses))), losses
-    assert losses[-1] < 0.9 * losses[0], losses
+    # monotone decrease from the first AdamW step on (the first two entries are the same weights)
+    assert all(b < a for a, b in zip(losses[1:], losses[2:])), losses
+    assert losses[-1] < 0.95 * losses[0], losses
