@@ -248,12 +248,16 @@ static hipError_t launch_chain(const ChainArgs& a, bool bwd, hipStream_t s) {
     case 48: return launch_chain_d<48>(a, bwd, s);
     case 64: return launch_chain_d<64>(a, bwd, s);
     case 128: return launch_chain_d<128>(a, bwd, s);
-    case 256: return launch_chain_d<256>(a, bwd, s);
     default: return hipErrorInvalidValue;
   }
 }
 
-hipError_t launch_chain_fwd(const ChainArgs& a, hipStream_t s) { return launch_chain(a, false, s); }
-hipError_t launch_chain_bwd(const ChainArgs& a, hipStream_t s) { return launch_chain(a, true, s); }
+// d = 256 runs on chain2.hip (output-major bf16x6 in both directions; the engine packs its images)
+hipError_t launch_chain_fwd(const ChainArgs& a, hipStream_t s) {
+  return a.D == 256 ? launch_chain2(a, false, s) : launch_chain(a, false, s);
+}
+hipError_t launch_chain_bwd(const ChainArgs& a, hipStream_t s) {
+  return a.D == 256 ? launch_chain2(a, true, s) : launch_chain(a, true, s);
+}
 
 }  // namespace gnot

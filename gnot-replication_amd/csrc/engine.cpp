@@ -396,6 +396,9 @@ static void plan_images(gnot_plan* p) {
     // remember which linear: encode in W/b later
     p->pack_jobs.back().W = reinterpret_cast<const float*>((intptr_t)li);
   };
+  // d = 256: chain2.hip, bf16x6 output-major images in both directions; else chain.hip, k-major x6
+  // forward image + exact fp32 backward-data image
+  const bool c2 = p->D == 256;
   auto chain_imgs = [&](int first, int KT0, int OTL) {
     for (int j = 0; j < NL; ++j) {
       const int li = first + j;
@@ -403,9 +406,9 @@ static void plan_images(gnot_plan* p) {
       const int OTp = (j == NL - 1) ? OTL : DT;
       Img f = new_img_x6(OTp, KTp);
       const size_t bo = new_bias(16 * OTp);
-      job(li, f, 0, 0, OTp, KTp, 0, (long)bo, 1);
-      Img t = new_img(KTp, OTp);          // backward-data image: exact fp32 MFMA (chain_bwd)
-      job(li, t, 0, 0, KTp, OTp, 1, -1);
+      job(li, f, 0, 0, OTp, KTp, 0, (long)bo, c2 ? 2 : 1);
+      Img t = c2 ? new_img_x6(KTp, OTp) : new_img(KTp, OTp);   // backward-data image
+      job(li, t, 0, 0, KTp, OTp, 1, -1, c2 ? 2 : 0);
       p->fwd_img[li] = f;
       p->T_img[li] = t;
       p->fwd_bias[li] = bo;

@@ -21,7 +21,8 @@ struct PackJob {
   int transposed;
   int o0, t0, ktot;
   int OTp, KTp;        // tile counts of this job's image (>= what out/in need; the rest is zero)
-  int x6;              // 1: bf16x6 image (3 bf16 pieces per 16x32 block, k-major, gnot_common.h), else fp32
+  int x6;              // 1: bf16x6 image (3 bf16 pieces per 16x32 block, k-major, gnot_common.h); 2: the
+                       //    same output-major (chain2.hip); 0: fp32
   int otot;            // x6: output tiles of the whole image (its k-major block stride)
 };
 // pack tiles of a job: fp32 images have OTp*KTp tiles, x6 images OTp*ceil(KTp/2) blocks
@@ -82,6 +83,9 @@ struct ChainArgs {
 };
 hipError_t launch_chain_fwd(const ChainArgs& a, hipStream_t s);
 hipError_t launch_chain_bwd(const ChainArgs& a, hipStream_t s);
+// d = 256 chains (chain2.hip): bf16x6 in both directions, output-major x6 images (pack x6 = 2) for Wp
+// AND WpT
+hipError_t launch_chain2(const ChainArgs& a, bool bwd, hipStream_t s);
 
 // ------------------------------------------------------------------ point-reduction GEMM (wgrad.hip)
 // C[out, in] = sum_p dz[p, :out]^T x[p, :in] over a point range, plus column sums of dz.

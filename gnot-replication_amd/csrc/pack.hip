@@ -28,7 +28,9 @@ __global__ void __launch_bounds__(64) pack_kernel(const PackJob* __restrict__ jo
   const int lane = threadIdx.x;
   const int r16 = lane & 15, g = lane >> 4;
   if (J.x6) {
-    // bf16x6 image block (o, kb), k-major: lane holds row 16o + r16 at k-slots 8g + j of k-block kb
+    // bf16x6 image block (o, kb): lane holds row 16o + r16 at k-slots 8g + j of k-block kb; blocks are
+    // k-major (x6 = 1: chain.hip, a k-block of every output tile together) or output-major (x6 = 2:
+    // chain2.hip, an output tile's k-blocks together)
     const int KB = (J.KTp + 1) / 2;
     const int o = t / KB, kb = t % KB;
     unsigned w[3][8];
@@ -55,7 +57,9 @@ __global__ void __launch_bounds__(64) pack_kernel(const PackJob* __restrict__ jo
       u.y = (w[q][3] & 0xFFFF0000u) | (w[q][2] >> 16);
       u.z = (w[q][5] & 0xFFFF0000u) | (w[q][4] >> 16);
       u.w = (w[q][7] & 0xFFFF0000u) | (w[q][6] >> 16);
-      dst[((long)(J.t0 / 2 + kb) * J.otot + J.o0 + o) * 3 * WAVE + q * WAVE + lane] = u;
+      const long blk = J.x6 == 2 ? (long)(J.o0 + o) * ((J.ktot + 1) / 2) + J.t0 / 2 + kb    // output-major
+                                 : (long)(J.t0 / 2 + kb) * J.otot + J.o0 + o;               // k-major
+      dst[blk * 3 * WAVE + q * WAVE + lane] = u;
     }
     if (J.bias_dst && t == 0) {
       const int nb = 16 * J.OTp;
