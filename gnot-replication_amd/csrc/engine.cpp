@@ -420,19 +420,24 @@ static void plan_images(gnot_plan* p) {
   for (int i = 0; i < p->I; ++i) chain_imgs(p->lin_fn(i, 0), kt_of(p->F), DT);
   p->cross_img.assign(p->L, gnot_plan::AttnImgs());
   p->self_img.assign(p->L, gnot_plan::AttnImgs());
+  // attention projections: at d = 256 the q | q|k|v | fc_out images and the backward-data images that
+  // linear2.hip uses are output-major bf16x6; the input-function K/V images and their backward-data
+  // images stay fp32 for the batched linear.hip kernel
   auto attn_imgs = [&](gnot_plan::AttnImgs& A, int iq, int io, const std::vector<int>& ik,
                        const std::vector<int>& iv, bool selftype) {
     const int D = p->D;
+    const int x6 = c2 ? 2 : 0;
+    auto img = [&](int OT, int KT) { return c2 ? new_img_x6(OT, KT) : new_img(OT, KT); };
     if (selftype) {
-      A.qkv = new_img(3 * DT, DT);
+      A.qkv = img(3 * DT, DT);
       A.bqkv = new_bias(3 * D);
-      job(iq, A.qkv, 0, 0, DT, DT, 0, (long)A.bqkv);
-      job(ik[0], A.qkv, DT, 0, DT, DT, 0, (long)(A.bqkv + D));
-      job(iv[0], A.qkv, 2 * DT, 0, DT, DT, 0, (long)(A.bqkv + 2 * D));
+      job(iq, A.qkv, 0, 0, DT, DT, 0, (long)A.bqkv, x6);
+      job(ik[0], A.qkv, DT, 0, DT, DT, 0, (long)(A.bqkv + D), x6);
+      job(iv[0], A.qkv, 2 * DT, 0, DT, DT, 0, (long)(A.bqkv + 2 * D), x6);
     } else {
-      A.q = new_img(DT, DT);
+      A.q = img(DT, DT);
       A.bq = new_bias(D);
-      job(iq, A.q, 0, 0, DT, DT, 0, (long)A.bq);
+      job(iq, A.q, 0, 0, DT, DT, 0, (long)A.bq, x6);
       for (size_t i = 0; i < ik.size(); ++i) {
         Img kv = new_img(2 * DT, DT);
         const size_t bkv = new_bias(2 * D);
@@ -442,17 +447,23 @@ static void plan_images(gnot_plan* p) {
         A.bkv.push_back(bkv);
       }
     }
-    A.o = new_img(DT, DT);
+    A.o = img(DT, DT);
     A.bo = new_bias(D);
-    job(io, A.o, 0, 0, DT, DT, 0, (long)A.bo);
-    std::vector<int> all = {iq, io};
-    all.insert(all.end(), ik.begin(), ik.end());
-    all.insert(all.end(), iv.begin(), iv.end());
-    for (int li : all) {
-      Img t = new_img(DT, DT);
-      job(li, t, 0, 0, DT, DT, 1, -1);
+    job(io, A.o, 0, 0, DT, DT, 0, (long)A.bo, x6);
+    std::vector<int> mine = {iq, io};
+    if (selftype) { mine.push_back(ik[0]); mine.push_back(iv[0]); }
+    for (int li : mine) {
+      Img t = img(DT, DT);
+      job(li, t, 0, 0, DT, DT, 1, -1, x6);
       p->T_img[li] = t;
     }
+    if (!selftype)                          // input-function keys/values: batched fp32 kernel
+      for (size_t i = 0; i < ik.size(); ++i)
+        for (int li : {ik[i], iv[i]}) {
+          Img t = new_img(DT, DT);
+          job(li, t, 0, 0, DT, DT, 1, -1);
+          p->T_img[li] = t;
+        }
   };
   for (int l = 0; l < p->L; ++l) {
     std::vector<int> ck, cv;
@@ -1282,7 +1293,7 @@ int run_linear(Ctx& c, const float* X, long ldx, int K, const Img& A, const floa
   a.nseg = 1; a.X[0] = X; a.Wp[0] = A.p; a.ldx = ldx; a.nsum = 1; a.sum_stride = 0; a.K = K;
   a.bias = bias; a.Y = Y; a.ldy = ldy; a.NO = NO; a.P = (int)P;
   a.epi = epi; a.nsoft = nsoft; a.dh = c.p->dh;
-  GNOT_CK(launch_linear(a, c.p->D, c.s));
+  GNOT_CK(c.p->D == 256 ? launch_linear2(a, c.s) : launch_linear(a, c.p->D, c.s));
   return GNOT_OK;
 }
 
@@ -1298,7 +1309,7 @@ int run_linear_seg(Ctx& c, std::initializer_list<std::pair<const float*, const I
   }
   a.ldx = ldx; a.nsum = 1; a.K = c.p->D; a.bias = nullptr; a.Y = Y; a.ldy = ldy; a.NO = c.p->D; a.P = (int)P;
   a.epi = epi; a.nsoft = 0; a.dh = c.p->dh;
-  GNOT_CK(launch_linear(a, c.p->D, c.s));
+  GNOT_CK(c.p->D == 256 ? launch_linear2(a, c.s) : launch_linear(a, c.p->D, c.s));
   return GNOT_OK;
 }
 

@@ -51,6 +51,9 @@ struct LinearArgs {
   int dh;                            // head width for that softmax
 };
 hipError_t launch_linear(const LinearArgs& a, int D, hipStream_t s);
+// d = 256 projections on bf16x6 MFMA (linear2.hip): Wp[s] are OUTPUT-MAJOR x6 images (pack x6 = 2)
+bool linear2_supported(const LinearArgs& a, int D);
+hipError_t launch_linear2(const LinearArgs& a, hipStream_t s);
 // jobs_dev: device array of independent LinearArgs (same D and NO), one per grid.z
 hipError_t launch_linear_batch(const LinearArgs* jobs_dev, int njobs, int maxP, int NO, int D, int dh, hipStream_t s);
 

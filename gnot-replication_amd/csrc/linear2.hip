@@ -1,0 +1,166 @@
+// Attention projections at hidden width d = 256 on bf16x6 MFMA, output-major (x6_core.h):
+//   Y[p, :NO] (=|+=) epi( sum_s X_s[p, :256] . W_s^T + bias )
+// the query/key/value projections with the feature softmax of model.py:59/72/93 fused into the
+// epilogue (model.py:56, 67-68, 89-90), fc_out (model.py:106), and the backward-data products
+// dX = dY W of those Linears (dX = dQ Wq + dK Wk + dV Wv in one pass for the fused q|k|v).
+// 8 waves x 16 points per workgroup share one weight stream (one LDS chunk = one 16-column output
+// tile of an output-major x6 image); the input rows are loaded once and held as their exact bf16 split.
+//   linear2_kernel     one K-segment, any NO = 16 * OT: tiles are produced one head group (dh / 16
+//                      tiles) at a time and stored at once (softmax over the group when it lies in the
+//                      first nsoft columns).
+//   linear2_seg_kernel several K-segments (NO = 256): the 16 output tiles accumulate in registers
+//                      across the segments, one segment's input split at a time.
+#include "gnot_kernels.h"
+#include "x6_core.h"
+
+namespace gnot {
+
+template <int TPH>   // output tiles per softmax head (dh / 16)
+__global__ void __launch_bounds__(64 * kC2Waves) linear2_kernel(LinearArgs a) {
+  constexpr int DT = 16, KB = 8;
+  extern __shared__ __attribute__((aligned(16))) u32x4 c2lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const long p = ((long)blockIdx.x * kC2Waves + wave) * 16 + (lane & 15);
+  const bool valid = p < a.P;
+  const int OT = a.NO / 16;
+  const u32x4* W = reinterpret_cast<const u32x4*>(a.Wp[0]);
+  C2Stream st{c2lds, c2_tile_u4(KB), 0, wave, lane};
+  stage_image(reinterpret_cast<float4*>(c2lds), reinterpret_cast<const float4*>(W), c2_tile_u4(KB), kC2Waves, wave,
+              lane);
+  u32x4 bp[KB][3];
+  {
+    float x[DT][4];
+    load_rows<DT>(x, a.X[0], a.ldx, p, valid, a.K, lane);
+    c2_split<DT>(x, bp);
+  }
+  // bias of the next head group and the old output rows (EPI_ACCUM) are loaded one group ahead / before
+  // the MFMAs: a load placed after a barrier would expose its full latency on every tile
+  float4 bn[TPH];
+#pragma unroll
+  for (int k = 0; k < TPH; ++k) bn[k] = a.bias ? ld4(a.bias + 16 * k + 4 * g) : make_float4(0.f, 0.f, 0.f, 0.f);
+  const long pc = valid ? p : 0;
+  for (int o0 = 0; o0 < OT; o0 += TPH) {
+    float h[TPH][4];
+    float4 bc[TPH], old[TPH];
+#pragma unroll
+    for (int k = 0; k < TPH; ++k) {
+      bc[k] = bn[k];
+      if (a.bias && o0 + TPH < OT) bn[k] = ld4(a.bias + 16 * (o0 + TPH + k) + 4 * g);
+      if (a.epi == EPI_ACCUM) old[k] = ld4(a.Y + pc * a.ldy + 16 * (o0 + k) + 4 * g);
+    }
+#pragma unroll
+    for (int k = 0; k < TPH; ++k) {
+      const int o = o0 + k;
+      const u32x4* cb = st.begin(W, o, OT, c2_tile_u4(KB), nullptr, 0);
+      const f32x4 acc = c2_tile<KB>(cb, bp, f32x4{bc[k].x, bc[k].y, bc[k].z, bc[k].w}, lane);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) h[k][r] = acc[r];
+    }
+    if (16 * o0 < a.nsoft) {
+      // feature softmax over the head: TPH tiles x (4 features of each of the 4 lane groups)
+      float m = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < TPH; ++k) m = fmaxf(m, fmaxf(fmaxf(h[k][0], h[k][1]), fmaxf(h[k][2], h[k][3])));
+      m = fmaxf(m, shfl_xor(m, 16));
+      m = fmaxf(m, shfl_xor(m, 32));
+      float sum = 0.f;
+#pragma unroll
+      for (int k = 0; k < TPH; ++k)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { h[k][r] = __expf(h[k][r] - m); sum += h[k][r]; }
+      sum += shfl_xor(sum, 16);
+      sum += shfl_xor(sum, 32);
+      const float inv = 1.0f / sum;
+#pragma unroll
+      for (int k = 0; k < TPH; ++k)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) h[k][r] *= inv;
+    }
+    if (valid) {
+#pragma unroll
+      for (int k = 0; k < TPH; ++k) {
+        float4 v = make_float4(h[k][0], h[k][1], h[k][2], h[k][3]);
+        if (a.epi == EPI_ACCUM) { v.x += old[k].x; v.y += old[k].y; v.z += old[k].z; v.w += old[k].w; }
+        *reinterpret_cast<float4*>(a.Y + p * a.ldy + 16 * (o0 + k) + 4 * g) = v;
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(64 * kC2Waves) linear2_seg_kernel(LinearArgs a) {
+  constexpr int DT = 16, KB = 8;
+  extern __shared__ __attribute__((aligned(16))) u32x4 c2lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const long p = ((long)blockIdx.x * kC2Waves + wave) * 16 + (lane & 15);
+  const bool valid = p < a.P;
+  C2Stream st{c2lds, c2_tile_u4(KB), 0, wave, lane};
+  stage_image(reinterpret_cast<float4*>(c2lds), reinterpret_cast<const float4*>(a.Wp[0]), c2_tile_u4(KB), kC2Waves,
+              wave, lane);
+  f32x4 acc[DT];
+#pragma unroll
+  for (int o = 0; o < DT; ++o) {
+    if (a.bias) {
+      const float4 b = ld4(a.bias + 16 * o + 4 * g);
+      acc[o] = f32x4{b.x, b.y, b.z, b.w};
+    } else {
+      acc[o] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  for (int s = 0; s < a.nseg; ++s) {
+    u32x4 bp[KB][3];
+    {
+      float x[DT][4];
+      load_rows<DT>(x, a.X[s], a.ldx, p, valid, a.K, lane);
+      c2_split<DT>(x, bp);
+    }
+    const u32x4* W = reinterpret_cast<const u32x4*>(a.Wp[s]);
+    const u32x4* next = s + 1 < a.nseg ? reinterpret_cast<const u32x4*>(a.Wp[s + 1]) : nullptr;
+#pragma unroll
+    for (int o = 0; o < DT; ++o) {
+      const u32x4* cb = st.begin(W, o, DT, c2_tile_u4(KB), next, c2_tile_u4(KB));
+      acc[o] = c2_tile<KB, false>(cb, bp, acc[o], lane);
+    }
+  }
+  if (valid) {
+#pragma unroll
+    for (int o = 0; o < DT; ++o) {
+      float4* y = reinterpret_cast<float4*>(a.Y + p * a.ldy + 16 * o + 4 * g);
+      float4 v = make_float4(acc[o][0], acc[o][1], acc[o][2], acc[o][3]);
+      if (a.epi == EPI_ACCUM) {
+        const float4 old = *y;
+        v.x += old.x; v.y += old.y; v.z += old.z; v.w += old.w;
+      }
+      *y = v;
+    }
+  }
+}
+
+bool linear2_supported(const LinearArgs& a, int D) {
+  return D == 256 && a.K == 256 && a.nsum == 1 && a.NO % 16 == 0 && (a.ldx & 3) == 0 && (a.ldy & 3) == 0 &&
+         (a.nseg == 1 ? (a.nsoft == 0 || a.dh == 16 || a.dh == 32 || a.dh == 64) : (a.NO == 256 && a.nsoft == 0));
+}
+
+hipError_t launch_linear2(const LinearArgs& a, hipStream_t s) {
+  if (a.P <= 0) return hipSuccess;
+  if (!linear2_supported(a, 256)) return hipErrorInvalidValue;
+  const size_t lds = 2 * (size_t)c2_tile_u4(8) * 16;
+  const dim3 grid((a.P + 16 * kC2Waves - 1) / (16 * kC2Waves)), block(64 * kC2Waves);
+  static bool attr = false;
+  if (!attr) {
+    for (const void* f : {reinterpret_cast<const void*>(linear2_kernel<1>), reinterpret_cast<const void*>(linear2_kernel<2>),
+                          reinterpret_cast<const void*>(linear2_kernel<4>), reinterpret_cast<const void*>(linear2_seg_kernel)})
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  if (a.nseg > 1) {
+    hipLaunchKernelGGL(linear2_seg_kernel, grid, block, lds, s, a);
+  } else {
+    const int tph = a.nsoft ? a.dh / 16 : 2;
+    if (tph == 1) hipLaunchKernelGGL(linear2_kernel<1>, grid, block, lds, s, a);
+    else if (tph == 2) hipLaunchKernelGGL(linear2_kernel<2>, grid, block, lds, s, a);
+    else hipLaunchKernelGGL(linear2_kernel<4>, grid, block, lds, s, a);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace gnot

@@ -89,8 +89,16 @@ int main(int argc, char** argv) {
     LinearArgs l{};
     l.nseg = 1; l.X[0] = X; l.Wp[0] = W; l.ldx = D; l.nsum = 1; l.K = D; l.bias = bias; l.Y = Y; l.ldy = NO;
     l.NO = NO; l.P = P; l.epi = EPI_STORE; l.nsoft = 0; l.dh = 16;
-    t = time_us([&] { CK(launch_linear(l, D, nullptr)); });
+    t = time_us([&] { CK(D == 256 ? launch_linear2(l, nullptr) : launch_linear(l, D, nullptr)); });
     std::printf("linear     P=%d K=%d NO=%d: %8.2f us  %6.1f TFLOP/s\n", P, D, NO, t, 2.0 * P * D * NO / t / 1e6);
+    if (D == 256 && NO == D) {
+      l.epi = EPI_ACCUM;
+      t = time_us([&] { CK(launch_linear2(l, nullptr)); });
+      std::printf("linear     P=%d K=%d NO=%d accum: %8.2f us  %6.1f TFLOP/s\n", P, D, NO, t, 2.0 * P * D * NO / t / 1e6);
+      l.nseg = 3; l.X[1] = X; l.X[2] = X; l.Wp[1] = W; l.Wp[2] = W; l.bias = nullptr;
+      t = time_us([&] { CK(launch_linear2(l, nullptr)); });
+      std::printf("linear     P=%d K=3x%d NO=%d accum: %8.2f us  %6.1f TFLOP/s\n", P, D, NO, t, 6.0 * P * D * NO / t / 1e6);
+    }
   }
   {  // finite dZ for the weight-gradient runs (the chain_bwd above wrote arbitrary values)
     float* fresh = dalloc((size_t)E * NL * P * D, 0.5f);
