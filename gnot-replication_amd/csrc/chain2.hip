@@ -29,13 +29,16 @@ namespace gnot {
 // The epilogue of tile o-1 follows the MFMAs of tile o in program order (independent work the
 // scheduler can place between them).
 template <int OT, int KBI, bool GELU = true>
-GNOT_DEV void c2_fwd_layer(C2Stream& st, const u32x4* W, const u32x4 (&in)[KBI][3], const float* bias, float* sv,
-                           const u32x4* nextW, int next_u4, long p, bool valid, int g, int lane, int D,
+GNOT_DEV void c2_fwd_layer(C2Stream& st, const u32x4* W, const u32x4 (&in)[KBI][3], const float* bias, const float* sv,
+                           unsigned sv_bytes, int voff, const u32x4* nextW, int next_u4, int g, int lane,
                            float (&out)[OT][4]) {
+  // saved pre-activations through a buffer resource: base + bound in SGPRs, the lane's row offset in
+  // one VGPR, the tile in the immediate; tail lanes (rows past P) fall outside the bound and are dropped
+  const rsrc_t rs = make_rsrc(sv, sv ? sv_bytes : 0u);
   float4 bn = ld4(bias + 4 * g);
   f32x4 prev;
   auto epi = [&](int o, const f32x4& acc) {
-    if (sv && valid) *reinterpret_cast<float4*>(sv + p * D + 16 * o + 4 * g) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    if (sv) buf_store_f32x4(make_float4(acc[0], acc[1], acc[2], acc[3]), rs, voff + 64 * o, 0);
 #pragma unroll
     for (int r = 0; r < 4; ++r) out[o][r] = GELU ? gelu(acc[r]) : acc[r];
     pin4(out[o]);
@@ -45,7 +48,7 @@ GNOT_DEV void c2_fwd_layer(C2Stream& st, const u32x4* W, const u32x4 (&in)[KBI][
     const float4 bb = bn;
     if (o + 1 < OT) bn = ld4(bias + 16 * (o + 1) + 4 * g);
     const u32x4* cb = st.begin(W, o, OT, c2_tile_u4(KBI), nextW, next_u4);
-    const f32x4 acc = c2_tile<KBI, false>(cb, in, f32x4{bb.x, bb.y, bb.z, bb.w}, lane);
+    const f32x4 acc = c2_tile<KBI, true>(cb, in, f32x4{bb.x, bb.y, bb.z, bb.w}, lane);
     if (o > 0) epi(o - 1, prev);
     prev = acc;
   }
@@ -62,6 +65,8 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) 
   const int e = blockIdx.y, nl = a.nlin;
   const ChainLayer* L = a.layers + e * nl;
   float* save = a.save ? a.save + e * a.save_chain_stride : nullptr;
+  const unsigned lay_bytes = (unsigned)min((long)a.P * D * 4, 0xFFFFFFFFL);   // one [P, D] layer
+  const int voff = (int)((blockIdx.x * kC2Waves + wave) * 16 + (lane & 15)) * D * 4 + 16 * g;
   const u32x4* W0 = reinterpret_cast<const u32x4*>(L[0].Wp);
   C2Stream st{c2lds, c2_tile_u4(KB), 0, wave, lane};
   stage_image(reinterpret_cast<float4*>(c2lds), reinterpret_cast<const float4*>(W0), c2_tile_u4(KB0), kC2Waves, wave,
@@ -78,7 +83,7 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) 
     const float* bias = L[0].bias;
     const u32x4* nextW = reinterpret_cast<const u32x4*>(nl > 1 ? L[1].Wp : nullptr);
     const int next_u4 = c2_tile_u4(KB);
-    c2_fwd_layer<DT, KB0>(st, W0, b0, bias, save, nextW, next_u4, p, valid, g, lane, D, nx);
+    c2_fwd_layer<DT, KB0>(st, W0, b0, bias, save, lay_bytes, voff, nextW, next_u4, g, lane, nx);
   }
   // ---- hidden layers 1 .. nl-2
   for (int l = 1; l < nl - 1; ++l) {
@@ -87,7 +92,7 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) 
     const u32x4* nextW = reinterpret_cast<const u32x4*>(L[l + 1].Wp);
     const float* bias = L[l].bias;
     float* sv = save ? save + l * a.save_layer_stride : nullptr;
-    c2_fwd_layer<DT, KB>(st, Wl, bp, bias, sv, nextW, c2_tile_u4(KB), p, valid, g, lane, D, nx);
+    c2_fwd_layer<DT, KB>(st, Wl, bp, bias, sv, lay_bytes, voff, nextW, c2_tile_u4(KB), g, lane, nx);
   }
   // ---- last layer (OTL output tiles)
   float y[OTL][4];
@@ -96,7 +101,7 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) 
     const u32x4* Wl = reinterpret_cast<const u32x4*>(L[nl - 1].Wp);
     const float* bias = L[nl - 1].bias;
     float* sv = save ? save + (nl - 1) * a.save_layer_stride : nullptr;
-    c2_fwd_layer<OTL, KB, false>(st, Wl, bp, bias, sv, nullptr, 0, p, valid, g, lane, D, y);
+    c2_fwd_layer<OTL, KB, false>(st, Wl, bp, bias, sv, lay_bytes, voff, nullptr, 0, g, lane, y);
   }
   if (a.mode == CH_SOFTMAX) {
     // softmax over the first out_dim outputs (features 16T + 4g + r); padded features excluded
@@ -142,7 +147,6 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
   const long p = ((long)blockIdx.x * kC2Waves + wave) * 16 + (lane & 15);
   const bool valid = p < a.P;
-  const long pc = valid ? p : 0;                     // clamped row for the (discarded) loads of tail lanes
   const int e = blockIdx.y, nl = a.nlin;
   const ChainLayer* L = a.layers + e * nl;
   const float* save = a.save + e * a.save_chain_stride;
@@ -197,11 +201,15 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) 
   u32x4 bp[KB][3];
   // one backward layer: g = W_l^T dz_l (DT output tiles), dz_{l-1} = g * gelu'(h_{l-1}) stored and kept
   // in nx; the saved pre-activation tile of o+1 is loaded while tile o's MFMAs run
+  const unsigned lay_bytes = (unsigned)min((long)a.P * D * 4, 0xFFFFFFFFL);   // one [P, D] layer
+  const int voff = (int)((blockIdx.x * kC2Waves + wave) * 16 + (lane & 15)) * D * 4 + 16 * g;
   auto layer = [&](const u32x4* Wt, const auto& in, int l, const u32x4* nextW, int next_u4) {
     constexpr int KBI = std::extent<std::remove_reference_t<decltype(in)>>::value;
-    const float* hs = save + (l - 1) * a.save_layer_stride + pc * D + 4 * g;
-    float* dzo = dz ? dz + (l - 1) * a.dz_layer_stride + p * D + 4 * g : nullptr;
-    float4 hn = ld4(hs);
+    // saved pre-activation h_{l-1} (read, one tile ahead) and dz_{l-1} (written) through buffer
+    // resources: rows past P read 0 / are dropped
+    const rsrc_t rh = make_rsrc(save + (l - 1) * a.save_layer_stride, lay_bytes);
+    const rsrc_t rz = make_rsrc(dz ? dz + (l - 1) * a.dz_layer_stride : nullptr, dz ? lay_bytes : 0u);
+    float4 hn = buf_load_f32x4(rh, voff, 0);
     f32x4 prev;
     float4 hp;
     auto epi = [&](int o, const f32x4& acc, const float4& hc) {
@@ -209,13 +217,13 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) 
       nx[o][1] = acc[1] * gelu_grad(hc.y);
       nx[o][2] = acc[2] * gelu_grad(hc.z);
       nx[o][3] = acc[3] * gelu_grad(hc.w);
-      if (dzo && valid) *reinterpret_cast<float4*>(dzo + 16 * o) = make_float4(nx[o][0], nx[o][1], nx[o][2], nx[o][3]);
+      if (dz) buf_store_f32x4(make_float4(nx[o][0], nx[o][1], nx[o][2], nx[o][3]), rz, voff + 64 * o, 0);
       pin4(nx[o]);
     };
 #pragma unroll
     for (int o = 0; o < DT; ++o) {
       const float4 hc = hn;
-      if (o + 1 < DT) hn = ld4(hs + 16 * (o + 1));
+      if (o + 1 < DT) hn = buf_load_f32x4(rh, voff + 64 * (o + 1), 0);
       const u32x4* cb = st.begin(Wt, o, DT, c2_tile_u4(KBI), nextW, next_u4);
       const f32x4 acc = c2_tile<KBI, false>(cb, in, f32x4{0.f, 0.f, 0.f, 0.f}, lane);
       if (o > 0) epi(o - 1, prev, hp);

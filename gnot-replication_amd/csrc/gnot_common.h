@@ -145,10 +145,14 @@ typedef __attribute__((address_space(1))) const void* global_cvoid_ptr;
 // that hands DMA'd LDS to other waves is preceded by this wait.
 GNOT_DEV void lds_dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// copy n4 float4 (a multiple of 64) from global to LDS; all threads of the workgroup call this
+// copy n4 float4 (a multiple of 64) from global to LDS; all threads of the workgroup call this.
+// Buffer form: the source base in SGPRs (one descriptor per copy), the lane's 16-byte offset in one
+// VGPR and the wave-instruction's base in soffset -- no 64-bit per-lane addresses to keep alive.
 GNOT_DEV void stage_image(float4* lds, const float4* __restrict__ g, int n4, int nwaves, int wave, int lane) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(g), (short)0, n4 * 16, 0x00020000);
   for (int base = wave * WAVE; base < n4; base += nwaves * WAVE)
-    __builtin_amdgcn_global_load_lds((global_cvoid_ptr)(g + base + lane), (lds_void_ptr)(lds + base), 16, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_ptr)(lds + base), 16, lane * 16, base * 16, 0, 0);
 }
 
 // acc[o] (o < OT) += W x in  with W (OT x KT tiles, packed) streamed through the LDS buffer `lds`
@@ -307,6 +311,13 @@ GNOT_DEV rsrc_t make_rsrc(const void* p, unsigned bytes) {
 }
 GNOT_DEV float buf_load_f32(rsrc_t r, int voff, int soff) {
   return u2f(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+GNOT_DEV float4 buf_load_f32x4(rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+// stores past the resource's `bytes` are dropped (tail lanes need no predicate)
+GNOT_DEV void buf_store_f32x4(float4 v, rsrc_t r, int voff, int soff) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, voff, soff, 0);
 }
 
 // exact 3-piece truncation split of 8 floats: p[q] = 8 bf16 (4 dwords, element j in the low half
