@@ -21,8 +21,9 @@
 //   attn_apply_fwd  res (head-major)
 //   attn_apply_bwd  du_i, dden_i per source, d(pre-softmax q)
 //   attn_kv_bwd     d(pre-softmax k), dv from (dS, dz)
-// The cross-point reductions themselves (S, z forward; dS, dz backward) are point-reduction GEMMs
-// on the MFMA path (wgrad.hip, state jobs), one job per sample.
+// The cross-point reductions themselves (S, z forward; dS, dz backward) are state.hip's
+// state_partial + state_reduce (per-head fp32 VALU blocks over LDS-staged rows, fixed-order
+// reduction of per-workgroup partials), one job per sample.
 #include "gnot_common.h"
 #include "gnot_kernels.h"
 

@@ -24,85 +24,111 @@
 
 namespace gnot {
 
+// LDS of one workgroup (u32x4 units): two weight-chunk buffers, two 1 KiB bias buffers (layer parity,
+// forward) and per wave four 1 KiB slots of saved pre-activation tiles (backward).
+template <int D>
+struct C2Lds {
+  static constexpr int WB = c2_tile_u4(D / 32);         // one output tile of a D x D x6 image
+  static constexpr int kBias = 2 * WB;                  // offset of the bias buffers
+  static constexpr int kHs = kBias + 2 * 64;            // offset of the saved-row slots
+  static constexpr int kBytes = (kHs + kC2Waves * 4 * 64) * 16;
+};
+
+struct C2Pipe {
+  u32x4* lds;
+  int WB;
+  int cnt;          // weight chunks consumed (buffer parity)
+  int wave, lane;
+  GNOT_DEV const u32x4* cur() const { return lds + (cnt & 1) * WB; }
+  GNOT_DEV u32x4* nxt() const { return lds + ((cnt + 1) & 1) * WB; }
+};
+
 // ------------------------------------------------------------------------------------------ forward
-// one forward layer: OT output tiles h = W a + b; saves h (if sv) and returns gelu(h) (GELU) or h in out.
-// The epilogue of tile o-1 follows the MFMAs of tile o in program order (independent work the
-// scheduler can place between them).
-template <int OT, int KBI, bool GELU = true>
-GNOT_DEV void c2_fwd_layer(C2Stream& st, const u32x4* W, const u32x4 (&in)[KBI][3], const float* bias, const float* sv,
-                           unsigned sv_bytes, int voff, const u32x4* nextW, int next_u4, int g, int lane,
-                           float (&out)[OT][4]) {
-  // saved pre-activations through a buffer resource: base + bound in SGPRs, the lane's row offset in
-  // one VGPR, the tile in the immediate; tail lanes (rows past P) fall outside the bound and are dropped
-  const rsrc_t rs = make_rsrc(sv, sv ? sv_bytes : 0u);
-  float4 bn = ld4(bias + 4 * g);
+// One forward layer: OT output tiles h = W a + b of the split input `in`; saves h (SAVE) and returns
+// gelu(h) (GELU) or h.  Entry: this layer's tile-0 weights sit in pp.cur() and its bias in bias buffer
+// `bsel`, DMA'd before exactly `pend0` later vector-memory ops of this wave.  Per tile o: counted wait
+// + barrier, DMA of tile o+1 (or of the next layer's bias then tile 0), the 6 x KB MFMAs, then the
+// epilogue of tile o-1 (its save store is the ONLY vector-memory op after the DMA, so the next wait is
+// vmcnt(1)).
+template <int OT, int KBI, bool GELU, bool SAVE>
+GNOT_DEV void c2f_layer(C2Pipe& pp, const u32x4* W, const u32x4 (&in)[KBI][3], int bsel, rsrc_t rs, int voff,
+                        const u32x4* nextW, int next_n16, const float* next_bias, int next_bias_bytes, int pend0,
+                        int g, float (&out)[OT][4]) {
+  constexpr int TU = c2_tile_u4(KBI);
+  const u32x4* bias = pp.lds + C2Lds<256>::kBias + bsel * 64;
   f32x4 prev;
   auto epi = [&](int o, const f32x4& acc) {
-    if (sv) buf_store_f32x4(make_float4(acc[0], acc[1], acc[2], acc[3]), rs, voff + 64 * o, 0);
+    if (SAVE) buf_store_f32x4(make_float4(acc[0], acc[1], acc[2], acc[3]), rs, voff + 64 * o);
 #pragma unroll
     for (int r = 0; r < 4; ++r) out[o][r] = GELU ? gelu(acc[r]) : acc[r];
     pin4(out[o]);
   };
 #pragma unroll
   for (int o = 0; o < OT; ++o) {
-    const float4 bb = bn;
-    if (o + 1 < OT) bn = ld4(bias + 16 * (o + 1) + 4 * g);
-    const u32x4* cb = st.begin(W, o, OT, c2_tile_u4(KBI), nextW, next_u4);
-    const f32x4 acc = c2_tile<KBI, true>(cb, in, f32x4{bb.x, bb.y, bb.z, bb.w}, lane);
+    if (o == 0) c2_sync_n(pend0);
+    else c2_sync_n((SAVE && o >= 2) ? 1 : 0);
+    const u32x4* cb = pp.cur();
+    if (o + 1 < OT) {
+      dma_image(pp.nxt(), W + (size_t)(o + 1) * TU, TU, kC2Waves, pp.wave, pp.lane);
+    } else if (nextW) {
+      // the next layer's bias first: the next layer's first wait only counts ops after its weights
+      if (pp.wave == 0)
+        dma16(make_rsrc(next_bias, (unsigned)next_bias_bytes), pp.lds + C2Lds<256>::kBias + (bsel ^ 1) * 64,
+              pp.lane * 16, 0);
+      dma_image(pp.nxt(), nextW, next_n16, kC2Waves, pp.wave, pp.lane);
+    }
+    ++pp.cnt;
+    const u32x4 bb = bias[4 * o + g];
+    const f32x4 acc = c2_tile<KBI, false>(cb, in, __builtin_bit_cast(f32x4, bb), pp.lane);
     if (o > 0) epi(o - 1, prev);
     prev = acc;
   }
   epi(OT - 1, prev);
 }
 
-template <int D, int KT0, int OTL>
+template <int D, int KT0, int OTL, bool SAVE>
 __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) {
   constexpr int DT = D / 16, KB = DT / 2, KB0 = (KT0 + 1) / 2;
+  using LD = C2Lds<D>;
   extern __shared__ __attribute__((aligned(16))) u32x4 c2lds[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4;
   const long p = ((long)blockIdx.x * kC2Waves + wave) * 16 + (lane & 15);
   const bool valid = p < a.P;
   const int e = blockIdx.y, nl = a.nlin;
   const ChainLayer* L = a.layers + e * nl;
-  float* save = a.save ? a.save + e * a.save_chain_stride : nullptr;
+  float* save = SAVE ? a.save + e * a.save_chain_stride : nullptr;
   const unsigned lay_bytes = (unsigned)min((long)a.P * D * 4, 0xFFFFFFFFL);   // one [P, D] layer
   const int voff = (int)((blockIdx.x * kC2Waves + wave) * 16 + (lane & 15)) * D * 4 + 16 * g;
+  C2Pipe pp{c2lds, LD::WB, 0, wave, lane};
   const u32x4* W0 = reinterpret_cast<const u32x4*>(L[0].Wp);
-  C2Stream st{c2lds, c2_tile_u4(KB), 0, wave, lane};
-  stage_image(reinterpret_cast<float4*>(c2lds), reinterpret_cast<const float4*>(W0), c2_tile_u4(KB0), kC2Waves, wave,
-              lane);
+  if (wave == 0) dma16(make_rsrc(L[0].bias, 16 * DT * 4), c2lds + LD::kBias, lane * 16, 0);
+  dma_image(c2lds, W0, c2_tile_u4(KB0), kC2Waves, wave, lane);
+  auto wp = [&](int l) { return reinterpret_cast<const u32x4*>(L[l].Wp); };
+  auto rs = [&](int l) { return make_rsrc(SAVE ? save + l * a.save_layer_stride : nullptr, SAVE ? lay_bytes : 0u); };
+  constexpr int pend_next = SAVE ? 2 : 0;    // a layer's first wait: the previous layer's last two saves
 
   float nx[DT][4];                                   // next layer input (fp32), then split
   u32x4 bp[KB][3];
-  // ---- layer 0 (input: KT0 tiles of the chain input)
+  int bsel = 0;
   {
     float x0[KT0][4];
     load_rows<KT0>(x0, a.X, a.ldx, p, valid, a.in_dim, lane);
     u32x4 b0[KB0][3];
     c2_split<KT0>(x0, b0);
-    const float* bias = L[0].bias;
-    const u32x4* nextW = reinterpret_cast<const u32x4*>(nl > 1 ? L[1].Wp : nullptr);
-    const int next_u4 = c2_tile_u4(KB);
-    c2_fwd_layer<DT, KB0>(st, W0, b0, bias, save, lay_bytes, voff, nextW, next_u4, g, lane, nx);
+    const int nb = nl - 1 == 1 ? 16 * OTL * 4 : 16 * DT * 4;
+    c2f_layer<DT, KB0, true, SAVE>(pp, W0, b0, bsel, rs(0), voff, wp(1), c2_tile_u4(KB), L[1].bias, nb, 0, g, nx);
+    bsel ^= 1;
   }
-  // ---- hidden layers 1 .. nl-2
   for (int l = 1; l < nl - 1; ++l) {
     c2_split<DT>(nx, bp);
-    const u32x4* Wl = reinterpret_cast<const u32x4*>(L[l].Wp);
-    const u32x4* nextW = reinterpret_cast<const u32x4*>(L[l + 1].Wp);
-    const float* bias = L[l].bias;
-    float* sv = save ? save + l * a.save_layer_stride : nullptr;
-    c2_fwd_layer<DT, KB>(st, Wl, bp, bias, sv, lay_bytes, voff, nextW, c2_tile_u4(KB), g, lane, nx);
+    const int nb = l + 1 == nl - 1 ? 16 * OTL * 4 : 16 * DT * 4;
+    c2f_layer<DT, KB, true, SAVE>(pp, wp(l), bp, bsel, rs(l), voff, wp(l + 1), c2_tile_u4(KB), L[l + 1].bias, nb,
+                                  pend_next, g, nx);
+    bsel ^= 1;
   }
-  // ---- last layer (OTL output tiles)
   float y[OTL][4];
-  {
-    c2_split<DT>(nx, bp);
-    const u32x4* Wl = reinterpret_cast<const u32x4*>(L[nl - 1].Wp);
-    const float* bias = L[nl - 1].bias;
-    float* sv = save ? save + (nl - 1) * a.save_layer_stride : nullptr;
-    c2_fwd_layer<OTL, KB, false>(st, Wl, bp, bias, sv, lay_bytes, voff, nullptr, 0, g, lane, y);
-  }
+  c2_split<DT>(nx, bp);
+  c2f_layer<OTL, KB, false, SAVE>(pp, wp(nl - 1), bp, bsel, rs(nl - 1), voff, nullptr, 0, nullptr, 0, pend_next, g, y);
   if (a.mode == CH_SOFTMAX) {
     // softmax over the first out_dim outputs (features 16T + 4g + r); padded features excluded
     float m = -INFINITY;
@@ -140,22 +166,74 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) 
 }
 
 // ------------------------------------------------------------------------------------------ backward
+// One backward layer l: g = W_l^T dz_l (DT output tiles of the split input `in`), dz_{l-1} = g *
+// gelu'(h_{l-1}) stored (rz) and kept in nx.  The saved pre-activation tiles h_{l-1} arrive by LDS-DMA
+// two tiles ahead into this wave's four slots (tile o in slot o % 4; the next layer's tiles 0 and 1
+// are requested by this layer's last two tiles).  Entry: the layer's tile-0 weights in pp.cur(), its
+// h tiles 0 and 1 requested, `pend0` vector-memory ops issued after its tile-0 weight DMA.
+template <int KBI>
+GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][3], rsrc_t rh, rsrc_t rz, rsrc_t rh_next,
+                        bool has_next_h, int voff, const u32x4* nextW, int next_n16, int pend0, float (&nx)[16][4]) {
+  constexpr int DT = 16, TU = c2_tile_u4(KBI);
+  u32x4* slots = pp.lds + C2Lds<256>::kHs + pp.wave * 4 * 64;
+  f32x4 prev;
+  auto epi = [&](int o, const f32x4& acc) {
+    const float4 hc = lds_read16_sync(slots + (o & 3) * 64 + pp.lane);
+    nx[o][0] = acc[0] * gelu_grad(hc.x);
+    nx[o][1] = acc[1] * gelu_grad(hc.y);
+    nx[o][2] = acc[2] * gelu_grad(hc.z);
+    nx[o][3] = acc[3] * gelu_grad(hc.w);
+    buf_store_f32x4(make_float4(nx[o][0], nx[o][1], nx[o][2], nx[o][3]), rz, voff + 64 * o);
+    pin4(nx[o]);
+  };
+#pragma unroll
+  for (int o = 0; o < DT; ++o) {
+    // ops after the weight DMA this wait retires (issued one tile earlier): the h tile requested with
+    // it (none when that request would have been past the next layer) and the dz store of tile o-2
+    if (o == 0) c2_sync_n(pend0);
+    else if (o == 1) c2_sync<1>();
+    else if (o + 1 < DT || has_next_h) c2_sync<2>();
+    else c2_sync<1>();
+    const u32x4* cb = pp.cur();
+    if (o + 1 < DT) dma_image(pp.nxt(), Wt + (size_t)(o + 1) * TU, TU, kC2Waves, pp.wave, pp.lane);
+    else if (nextW) dma_image(pp.nxt(), nextW, next_n16, kC2Waves, pp.wave, pp.lane);
+    ++pp.cnt;
+    if (o + 2 < DT) dma16(rh, slots + ((o + 2) & 3) * 64, voff, 64 * (o + 2));
+    else if (has_next_h) dma16(rh_next, slots + ((o + 2) & 3) * 64, voff, 64 * (o + 2 - DT));
+    const f32x4 acc = c2_tile<KBI, false>(cb, in, f32x4{0.f, 0.f, 0.f, 0.f}, pp.lane);
+    if (o > 0) epi(o - 1, prev);
+    prev = acc;
+    __builtin_amdgcn_sched_barrier(0);      // no code motion across tiles (register pressure)
+  }
+  epi(DT - 1, prev);
+}
+
 template <int D, int KT0, int OTL>
 __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) {
   constexpr int DT = D / 16, KB = DT / 2, KBL = (OTL + 1) / 2;
+  using LD = C2Lds<D>;
   extern __shared__ __attribute__((aligned(16))) u32x4 c2lds[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4;
   const long p = ((long)blockIdx.x * kC2Waves + wave) * 16 + (lane & 15);
   const bool valid = p < a.P;
   const int e = blockIdx.y, nl = a.nlin;
   const ChainLayer* L = a.layers + e * nl;
   const float* save = a.save + e * a.save_chain_stride;
-  float* dz = a.dz ? a.dz + e * a.dz_chain_stride : nullptr;
-  const u32x4* WL = reinterpret_cast<const u32x4*>(L[nl - 1].WpT);
-  C2Stream st{c2lds, c2_tile_u4(KB), 0, wave, lane};
-  stage_image(reinterpret_cast<float4*>(c2lds), reinterpret_cast<const float4*>(WL), c2_tile_u4(KBL), kC2Waves, wave,
-              lane);
-
+  float* dz = a.dz + e * a.dz_chain_stride;
+  const unsigned lay_bytes = (unsigned)min((long)a.P * D * 4, 0xFFFFFFFFL);   // one [P, D] layer
+  const int voff = (int)((blockIdx.x * kC2Waves + wave) * 16 + (lane & 15)) * D * 4 + 16 * g;
+  C2Pipe pp{c2lds, LD::WB, 0, wave, lane};
+  auto wt = [&](int l) { return reinterpret_cast<const u32x4*>(L[l].WpT); };
+  auto rh = [&](int l) { return make_rsrc(save + l * a.save_layer_stride, lay_bytes); };   // h_l
+  auto rz = [&](int l) { return make_rsrc(dz + l * a.dz_layer_stride, lay_bytes); };      // dz_l
+  // prologue DMA: the last Linear's tile-0 weights and the first two h_{nl-2} tiles
+  dma_image(c2lds, wt(nl - 1), c2_tile_u4(KBL), kC2Waves, wave, lane);
+  {
+    u32x4* slots = c2lds + LD::kHs + wave * 4 * 64;
+    const rsrc_t r = rh(nl - 2);
+    dma16(r, slots, voff, 0);
+    dma16(r, slots + 64, voff, 64);
+  }
   // ---- gradient at the chain output
   float dy[OTL][4];
   if (a.mode == CH_MOE) {
@@ -195,66 +273,36 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) 
   } else {
     load_rows<OTL>(dy, a.dY, a.lddy, p, valid, a.out_dim, lane);
   }
-  if (dz) store_rows<OTL>(dy, dz + (nl - 1) * a.dz_layer_stride, D, p, valid, 16 * OTL, lane);
+  store_rows<OTL>(dy, dz + (nl - 1) * a.dz_layer_stride, D, p, valid, 16 * OTL, lane);
 
   float nx[DT][4];
   u32x4 bp[KB][3];
-  // one backward layer: g = W_l^T dz_l (DT output tiles), dz_{l-1} = g * gelu'(h_{l-1}) stored and kept
-  // in nx; the saved pre-activation tile of o+1 is loaded while tile o's MFMAs run
-  const unsigned lay_bytes = (unsigned)min((long)a.P * D * 4, 0xFFFFFFFFL);   // one [P, D] layer
-  const int voff = (int)((blockIdx.x * kC2Waves + wave) * 16 + (lane & 15)) * D * 4 + 16 * g;
-  auto layer = [&](const u32x4* Wt, const auto& in, int l, const u32x4* nextW, int next_u4) {
-    constexpr int KBI = std::extent<std::remove_reference_t<decltype(in)>>::value;
-    // saved pre-activation h_{l-1} (read, one tile ahead) and dz_{l-1} (written) through buffer
-    // resources: rows past P read 0 / are dropped
-    const rsrc_t rh = make_rsrc(save + (l - 1) * a.save_layer_stride, lay_bytes);
-    const rsrc_t rz = make_rsrc(dz ? dz + (l - 1) * a.dz_layer_stride : nullptr, dz ? lay_bytes : 0u);
-    float4 hn = buf_load_f32x4(rh, voff, 0);
-    f32x4 prev;
-    float4 hp;
-    auto epi = [&](int o, const f32x4& acc, const float4& hc) {
-      nx[o][0] = acc[0] * gelu_grad(hc.x);
-      nx[o][1] = acc[1] * gelu_grad(hc.y);
-      nx[o][2] = acc[2] * gelu_grad(hc.z);
-      nx[o][3] = acc[3] * gelu_grad(hc.w);
-      if (dz) buf_store_f32x4(make_float4(nx[o][0], nx[o][1], nx[o][2], nx[o][3]), rz, voff + 64 * o, 0);
-      pin4(nx[o]);
-    };
-#pragma unroll
-    for (int o = 0; o < DT; ++o) {
-      const float4 hc = hn;
-      if (o + 1 < DT) hn = buf_load_f32x4(rh, voff + 64 * (o + 1), 0);
-      const u32x4* cb = st.begin(Wt, o, DT, c2_tile_u4(KBI), nextW, next_u4);
-      const f32x4 acc = c2_tile<KBI, false>(cb, in, f32x4{0.f, 0.f, 0.f, 0.f}, lane);
-      if (o > 0) epi(o - 1, prev, hp);
-      prev = acc;
-      hp = hc;
-    }
-    epi(DT - 1, prev, hp);
-  };
-  // ---- last Linear (input: dy, OTL tiles)
+  // next image after layer l's tiles: layer l-1's W^T, or the first Linear's (dX) when l - 1 == 0
+  auto next_img = [&](int l) -> const u32x4* { return (l - 1 >= 1 || a.dX) ? wt(l - 1) : nullptr; };
   {
     u32x4 bl[KBL][3];
     c2_split<OTL>(dy, bl);
-    const u32x4* nextW = reinterpret_cast<const u32x4*>(nl - 2 >= 1 ? L[nl - 2].WpT : (a.dX ? L[0].WpT : nullptr));
-    const int next_u4 = c2_tile_u4(KB);
-    layer(WL, bl, nl - 1, nextW, next_u4);
+    const int l = nl - 1;
+    c2b_layer<KBL>(pp, wt(l), bl, rh(l - 1), rz(l - 1), rh(l >= 2 ? l - 2 : 0), l - 1 >= 1, voff, next_img(l),
+                   c2_tile_u4(KB), 0, nx);
   }
-  // ---- hidden Linears nl-2 .. 1
   for (int l = nl - 2; l >= 1; --l) {
     c2_split<DT>(nx, bp);
-    const u32x4* Wt = reinterpret_cast<const u32x4*>(L[l].WpT);
-    const u32x4* nextW = reinterpret_cast<const u32x4*>(l - 1 >= 1 ? L[l - 1].WpT : (a.dX ? L[0].WpT : nullptr));
-    layer(Wt, bp, l, nextW, c2_tile_u4(KB));
+    c2b_layer<KB>(pp, wt(l), bp, rh(l - 1), rz(l - 1), rh(l >= 2 ? l - 2 : 0), l - 1 >= 1, voff, next_img(l),
+                  c2_tile_u4(KB), 3, nx);
   }
-  // ---- first Linear: dX = W_0^T dz_0 (KT0 output tiles)
+  // ---- first Linear: dX = W_0^T dz_0 (KT0 output tiles); first wait: the last layer's two dz stores
   if (a.dX) {
     c2_split<DT>(nx, bp);
-    const u32x4* W0 = reinterpret_cast<const u32x4*>(L[0].WpT);
+    const u32x4* W0 = wt(0);
     float dx[KT0][4];
 #pragma unroll
     for (int o = 0; o < KT0; ++o) {
-      const u32x4* cb = st.begin(W0, o, KT0, c2_tile_u4(KB), nullptr, 0);
+      if (o == 0) c2_sync<2>();
+      else c2_sync<0>();
+      const u32x4* cb = pp.cur();
+      if (o + 1 < KT0) dma_image(pp.nxt(), W0 + (size_t)(o + 1) * c2_tile_u4(KB), c2_tile_u4(KB), kC2Waves, wave, lane);
+      ++pp.cnt;
       f32x4 acc = c2_tile<KB, false>(cb, bp, f32x4{0.f, 0.f, 0.f, 0.f}, lane);
 #pragma unroll
       for (int r = 0; r < 4; ++r) dx[o][r] = acc[r];
@@ -267,19 +315,22 @@ template <int D>
 static hipError_t launch_chain2_d(const ChainArgs& a, bool bwd, hipStream_t s) {
   constexpr int DT = D / 16;
   const dim3 grid((a.P + 16 * kC2Waves - 1) / (16 * kC2Waves), a.nchains), block(64 * kC2Waves);
-  const size_t lds = 2 * (size_t)c2_tile_u4(DT / 2) * 16;
+  const size_t lds = C2Lds<D>::kBytes;
 #define GNOT_C2_CASE(K0, OL)                                                                         \
   if (a.KT0 == K0 && a.OTL == OL) {                                                                  \
     static bool attr = false;                                                                        \
     if (!attr) {                                                                                     \
       (void)hipFuncSetAttribute(reinterpret_cast<const void*>(chain2_bwd_kernel<D, K0, OL>),         \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);               \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(chain2_fwd_kernel<D, K0, OL>),         \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(chain2_fwd_kernel<D, K0, OL, true>),   \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);               \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(chain2_fwd_kernel<D, K0, OL, false>),  \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);               \
       attr = true;                                                                                   \
     }                                                                                                \
     if (bwd) hipLaunchKernelGGL((chain2_bwd_kernel<D, K0, OL>), grid, block, lds, s, a);             \
-    else hipLaunchKernelGGL((chain2_fwd_kernel<D, K0, OL>), grid, block, lds, s, a);                 \
+    else if (a.save) hipLaunchKernelGGL((chain2_fwd_kernel<D, K0, OL, true>), grid, block, lds, s, a); \
+    else hipLaunchKernelGGL((chain2_fwd_kernel<D, K0, OL, false>), grid, block, lds, s, a);          \
     return hipGetLastError();                                                                        \
   }
   GNOT_C2_CASE(1, 1)

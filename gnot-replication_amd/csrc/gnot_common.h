@@ -306,8 +306,13 @@ GNOT_DEV float u2f(unsigned x) { return __builtin_bit_cast(float, x); }
 // ---- buffer loads: base + bound in SGPRs (reads past `bytes` return 0), wave-uniform row offset in
 // an SGPR (soffset), only the lane's column offset in a VGPR
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
+// (base and bound are wave-uniform by construction; readfirstlane tells the compiler so, otherwise a
+// descriptor built from a value it cannot prove uniform is used inside a waterfall loop)
 GNOT_DEV rsrc_t make_rsrc(const void* p, unsigned bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+  const unsigned long long a = reinterpret_cast<unsigned long long>(p);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  void* up = reinterpret_cast<void*>(((unsigned long long)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(up, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 GNOT_DEV float buf_load_f32(rsrc_t r, int voff, int soff) {
   return u2f(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
@@ -315,9 +320,13 @@ GNOT_DEV float buf_load_f32(rsrc_t r, int voff, int soff) {
 GNOT_DEV float4 buf_load_f32x4(rsrc_t r, int voff, int soff) {
   return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
-// stores past the resource's `bytes` are dropped (tail lanes need no predicate)
-GNOT_DEV void buf_store_f32x4(float4 v, rsrc_t r, int voff, int soff) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, voff, soff, 0);
+// stores past the resource's `bytes` are dropped (tail lanes need no predicate).
+// The whole offset goes in the VGPR and soffset stays the constant 0: a 128-bit buffer store whose
+// soffset is an SGPR is not padded by the compiler's hazard recognizer (ROCm 7.2) against a VALU
+// overwriting its data registers on the next cycle, and on gfx950 the tail lanes then store the new
+// value (measured: element 0 of lanes 12-15 of every 16, chain2 saves, DESIGN.md "store-data hazard").
+GNOT_DEV void buf_store_f32x4(float4 v, rsrc_t r, int voff) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, voff, 0, 0);
 }
 
 // exact 3-piece truncation split of 8 floats: p[q] = 8 bf16 (4 dwords, element j in the low half

@@ -64,6 +64,54 @@ struct C2Stream {
   }
 };
 
+// ---- counted LDS-DMA pipeline (chain2.hip) ------------------------------------------------------
+// hipcc drains every outstanding vector-memory op (vmcnt(0)) at a __syncthreads() or at the use of an
+// ordinary load while an LDS-DMA is in flight, which also waits for the epilogue stores issued just
+// before.  The chains therefore use ONLY LDS-DMA loads inside the tile loop (weights, bias, saved
+// pre-activations) and a raw barrier preceded by a COUNTED wait: vmcnt(N) with N = the vector-memory
+// ops this wave issued after the DMA that must have landed (in-order completion), so the last tile's
+// stores stay in flight across the barrier.
+template <int N>
+GNOT_DEV void c2_sync() {
+#ifdef GNOT_C2_SAFE
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#else
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+#endif
+}
+GNOT_DEV void c2_sync_n(int n) {   // n is wave-uniform and small
+#ifdef GNOT_C2_SAFE
+  n = 0;
+#endif
+  switch (n) {
+    case 0: c2_sync<0>(); break;
+    case 1: c2_sync<1>(); break;
+    case 2: c2_sync<2>(); break;
+    default: c2_sync<3>(); break;
+  }
+}
+// LDS read of a slot this wave filled by LDS-DMA and already waited for with a counted vmcnt: inline
+// asm, so hipcc does not insert its own vmcnt(0) for the DMA still in flight to OTHER buffers (it cannot
+// tell the addresses apart and would drain the whole pipeline)
+GNOT_DEV float4 lds_read16_sync(const u32x4* p) {
+  float4 v;
+  const unsigned a = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) u32x4*)p;
+  asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+// this wave's own LDS-DMA (lane l: 16 B at lds + l) from a buffer resource at byte offset voff + soff
+GNOT_DEV void dma16(rsrc_t r, u32x4* lds, int voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_ptr)lds, 16, voff, soff, 0, 0);
+}
+// n16 16-byte units (a multiple of 64) of an image, split over the workgroup's waves
+GNOT_DEV void dma_image(u32x4* lds, const void* src, int n16, int nwaves, int wave, int lane) {
+  const rsrc_t r = make_rsrc(src, (unsigned)n16 * 16u);
+  // the LDS base (M0) and soffset must be SGPRs: a wave index the compiler cannot prove uniform turns
+  // every DMA into a waterfall loop
+  const int w = __builtin_amdgcn_readfirstlane(wave);
+  for (int base = w * WAVE; base < n16; base += nwaves * WAVE) dma16(r, lds + base, lane * 16, base * 16);
+}
+
 template <int KT>
 GNOT_DEV void c2_split(const float (&v)[KT][4], u32x4 (&bp)[(KT + 1) / 2][3]) {
 #pragma unroll

@@ -57,6 +57,10 @@ def run(bwd):
     return sig(model.engine())
 
 
+if len(sys.argv) > 2:          # dump the signatures (compare two library builds across processes)
+    import json
+    json.dump({"fwd": run(False), "fwd+bwd": run(True)}, open(sys.argv[2], "w"))
+    sys.exit(0)
 for bwd in (False, True):
     a = run(bwd)
     b = run(bwd)
