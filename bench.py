@@ -397,9 +397,13 @@ def main():
                    "parallelism": (f"point-shard{world}" if shard else f"sample-dp{world}") if world > 1 else "single",
                    "step": "pack+fwd+RelL2+bwd+AdamW (native loss, " + ("torch fused AdamW" if args.torch_adamw else "native flat AdamW") + ")" + (" (hipGraph replay)" if use_graph else " (eager)")},
         "roofline": {
-            "kernel": {"moe_fwd": "chain_fwd_kernel (fused MoE expert chains, forward)",
-                       "moe_bwd": "chain_bwd_kernel (fused MoE expert chains, backward)",
-                       "wgrad": "pgemm_x6_kernel+pgemm_reduce_kernel (weight gradients, bf16x6 MFMA)"}[rkind],
+            "kernel": ({"moe_fwd": "chain2_fwd_kernel (fused MoE expert chains, forward, bf16x6 MFMA)",
+                        "moe_bwd": "chain2_bwd_kernel (fused MoE expert chains, backward, bf16x6 MFMA)",
+                        "wgrad": "pgemm_x6w_kernel+pgemm_reduce_kernel (weight gradients, 256x256 bf16x6 MFMA)"}
+                       if m["n_attn_hidden_dim"] == 256 else
+                       {"moe_fwd": "chain_fwd_kernel (fused MoE expert chains, forward)",
+                        "moe_bwd": "chain_bwd_kernel (fused MoE expert chains, backward)",
+                        "wgrad": "pgemm_x6_kernel+pgemm_reduce_kernel (weight gradients, bf16x6 MFMA)"})[rkind],
             "class": rkind,
             "class_ms_per_step": {k: round(v[0], 3) for k, v in kinds.items()},
             "bound": "mfma",
