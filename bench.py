@@ -146,6 +146,26 @@ def make_rank_batch(w, rank, world, device):
                 meshes=w["B"])
 
 
+def permuted_batch(D, k):
+    """The rank's variable-mesh batch with its meshes in the k-th seeded random order (new packed
+    offsets, same data): main.py:41's shuffle=True re-batching, which changes the geometry every step."""
+    B = D["B"]
+    order = torch.randperm(B, generator=torch.Generator(device="cpu").manual_seed(500 + k)).tolist()
+    xo, fo = D["x_off"], D["fn_offs"]
+    pick = lambda t, off: torch.cat([t[off[b]:off[b + 1]] for b in order])
+    x_off = [0]
+    for b in order:
+        x_off.append(x_off[-1] + xo[b + 1] - xo[b])
+    fn_offs = []
+    for o in fo:
+        n = [0]
+        for b in order:
+            n.append(n[-1] + o[b + 1] - o[b])
+        fn_offs.append(n)
+    return dict(x=pick(D["x"], xo), x_off=x_off, theta=D["theta"][order], y=pick(D["y"], xo),
+                fns=[pick(f, o) for f, o in zip(D["fns"], fo)], fn_offs=fn_offs)
+
+
 def make_batch(w, seed, device):
     g = torch.Generator(device="cpu").manual_seed(seed)
     m = w["model"]
@@ -217,6 +237,9 @@ def main():
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--torch-adamw", action="store_true", help="torch's fused AdamW instead of the native one")
     ap.add_argument("--breakdown", action="store_true", help="print per-kernel-class device time to stderr")
+    ap.add_argument("--vary-geometry", action="store_true",
+                    help="variable-mesh workloads: a new mesh order (hence new packed offsets) every step, as "
+                         "main.py:41's shuffled DataLoader does; eager launches")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -264,6 +287,13 @@ def main():
     x, x_off, theta, fns, fn_offs, y, seg, B = (D[k] for k in ("x", "x_off", "theta", "fns", "fn_offs", "y", "seg", "B"))
     eng = model.engine()
     eng.param_grads = bool(args.torch_adamw)      # the native AdamW reads the gradient arena directly
+    batches = None
+    if args.vary_geometry:
+        if not w.get("variable"):
+            raise SystemExit("--vary-geometry needs a variable-mesh workload (cfg5)")
+        batches = [permuted_batch(D, k) for k in range(max(args.warmup, 2) + 3 + args.steps)]
+        use_graph = False                         # every step binds a new geometry
+    it = {"k": 0}
     if shard:
         from gnot_amd import parallel as par
         model.set_point_shard(par.PointShardComm())
@@ -272,6 +302,11 @@ def main():
     # gradient buffer) -> [AdamW].  With hipGraphs the two bracketed parts are captured once and
     # replayed; the collective stays an eager RCCL call between them.
     def fwd_bwd():
+        nonlocal x, x_off, theta, fns, fn_offs, y
+        if batches is not None:
+            bt = batches[it["k"] % len(batches)]
+            it["k"] += 1
+            x, x_off, theta, fns, fn_offs, y = (bt[k] for k in ("x", "x_off", "theta", "fns", "fn_offs", "y"))
         out = model.forward_packed(x, x_off, theta, fns, fn_offs, n_global=D["n_global"])
         if shard:
             from gnot_amd import parallel as par
@@ -309,6 +344,7 @@ def main():
             eager_step()
     torch.cuda.current_stream(device).wait_stream(side)
     torch.cuda.synchronize()
+    print("[bench] warm-up done", file=sys.stderr, flush=True)
     # which kernel class dominates device time: one profiled eager step per class (untimed)
     kinds = {}
     for kind in ("moe_fwd", "moe_bwd", "wgrad"):
@@ -335,11 +371,13 @@ def main():
         torch.cuda.synchronize()
         eng.profile_enable(rkind)
         g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        print("[bench] capturing", file=sys.stderr, flush=True)
         with torch.cuda.graph(g_fb):
             fwd_bwd()
         with torch.cuda.graph(g_opt, pool=g_fb.pool()):
             opt_step()
         torch.cuda.synchronize()
+        print("[bench] captured", file=sys.stderr, flush=True)
 
         def graph_step():
             g_fb.replay()
@@ -394,6 +432,7 @@ def main():
                    "input_function_points": w["M"], "hidden": m["n_attn_hidden_dim"], "experts": m["n_expert"],
                    "heads": m["n_head"], "blocks": m["n_attn_layers"], "mlp_layers": m["n_mlp_num_layers"],
                    "input_functions": m["n_input_functions"],
+                   "geometry": "new mesh order every step (--vary-geometry)" if batches is not None else "fixed",
                    "parallelism": (f"point-shard{world}" if shard else f"sample-dp{world}") if world > 1 else "single",
                    "step": "pack+fwd+RelL2+bwd+AdamW (native loss, " + ("torch fused AdamW" if args.torch_adamw else "native flat AdamW") + ")" + (" (hipGraph replay)" if use_graph else " (eager)")},
         "roofline": {

@@ -149,6 +149,14 @@ struct gnot_plan {
   hipStream_t side2 = nullptr;          // input-function branch, concurrent with the query branch
   std::vector<hipEvent_t> evs;
   size_t ev_next = 0;
+  // pinned staging ring for the table uploads of gnot_plan_bind_workspace_async: slot k is rewritten
+  // only after the copy that last read it has executed (stage_ev[k])
+  static constexpr int kStageSlots = 4;
+  void* stage[kStageSlots] = {};
+  size_t stage_cap[kStageSlots] = {};
+  hipEvent_t stage_ev[kStageSlots] = {};
+  bool stage_used[kStageSlots] = {};
+  int stage_next = 0;
   std::map<const float*, hipEvent_t> readers;
   int4* d_qchunks = nullptr;
   int* d_qchunk_off = nullptr;
@@ -284,6 +292,13 @@ extern "C" void gnot_plan_destroy(gnot_plan* plan) {
   if (!plan) return;
   for (hipEvent_t e : plan->prof_events) (void)hipEventDestroy(e);
   for (hipEvent_t e : plan->evs) (void)hipEventDestroy(e);
+  for (int k = 0; k < gnot_plan::kStageSlots; ++k) {
+    if (plan->stage_ev[k]) {
+      (void)hipEventSynchronize(plan->stage_ev[k]);
+      (void)hipEventDestroy(plan->stage_ev[k]);
+    }
+    if (plan->stage[k]) (void)hipHostFree(plan->stage[k]);
+  }
   if (plan->side) (void)hipStreamDestroy(plan->side);
   if (plan->side2) (void)hipStreamDestroy(plan->side2);
   delete plan;
@@ -1121,7 +1136,18 @@ extern "C" int gnot_plan_grad_offsets(const gnot_plan* p, int64_t* grad_off) {
 }
 
 // ====================================================================== bind
+extern "C" int gnot_plan_bind_workspace_async(gnot_plan* p, void* workspace, size_t bytes, void* stream);
 extern "C" int gnot_plan_bind_workspace(gnot_plan* p, void* workspace, size_t bytes) {
+  const int rc = gnot_plan_bind_workspace_async(p, workspace, bytes, nullptr);
+  if (rc != GNOT_OK) return rc;
+  GNOT_CK(hipStreamSynchronize(nullptr));
+  return GNOT_OK;
+}
+
+// Stream-ordered bind: the table image goes through a pinned staging slot and one hipMemcpyAsync on
+// `stream`, so a new batch geometry costs no host synchronisation (the copy is ordered after the
+// previous step's kernels on that stream, which have joined every side stream by then).
+extern "C" int gnot_plan_bind_workspace_async(gnot_plan* p, void* workspace, size_t bytes, void* stream) {
   if (!p || !p->batch_set) return fail(GNOT_E_STATE, "set_batch first");
   if (!p->params_bound) return fail(GNOT_E_STATE, "bind_params first");
   if (!workspace || bytes < p->ws_need) return fail(GNOT_E_WORKSPACE, "workspace missing or too small");
@@ -1223,7 +1249,25 @@ extern "C" int gnot_plan_bind_workspace(gnot_plan* p, void* workspace, size_t by
   p->d_xsend_prefix = static_cast<int*>(put(p->xsend_prefix.data(), p->xsend_prefix.size() * sizeof(int)));
   p->d_xrecv_prefix = static_cast<int*>(put(p->xrecv_prefix.data(), p->xrecv_prefix.size() * sizeof(int)));
   if (cur > p->table_bytes) return fail(GNOT_E_INVALID, "internal: table overflow");
-  GNOT_CK(hipMemcpy(tp, host.data(), cur, hipMemcpyHostToDevice));
+  {
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    const int k = p->stage_next;
+    p->stage_next = (k + 1) % gnot_plan::kStageSlots;
+    if (!p->stage_ev[k]) GNOT_CK(hipEventCreateWithFlags(&p->stage_ev[k], hipEventDisableTiming));
+    if (p->stage_used[k]) GNOT_CK(hipEventSynchronize(p->stage_ev[k]));   // only when the ring wraps in flight
+    if (p->stage_cap[k] < cur) {
+      if (p->stage[k]) GNOT_CK(hipHostFree(p->stage[k]));
+      p->stage[k] = nullptr;
+      p->stage_cap[k] = 0;
+      const size_t cap = cur + cur / 2 + 4096;                           // headroom: growth is rare
+      GNOT_CK(hipHostMalloc(&p->stage[k], cap, hipHostMallocDefault));
+      p->stage_cap[k] = cap;
+    }
+    std::memcpy(p->stage[k], host.data(), cur);
+    GNOT_CK(hipMemcpyAsync(tp, p->stage[k], cur, hipMemcpyHostToDevice, s));
+    GNOT_CK(hipEventRecord(p->stage_ev[k], s));
+    p->stage_used[k] = true;
+  }
   if (!p->side2) GNOT_CK(hipStreamCreateWithFlags(&p->side2, hipStreamNonBlocking));
   if (!p->side) {
     // same priority as the caller's stream: measured on MI355X, a low- (or high-) priority side
@@ -1357,9 +1401,14 @@ int run_wgrad_side(Ctx& c, const WgradGroup& G, std::initializer_list<const floa
   if (G.jobs.empty()) return GNOT_OK;
   gnot_plan* p = c.p;
   static const bool serial = std::getenv("GNOT_SERIAL_WGRAD") != nullptr;   // diagnostics: no overlap
-  // only the caller's stream forks to the side stream (a fork from another forked stream is not
-  // captured correctly into a hipGraph on ROCm 7: capture_end faults); other streams run their
-  // weight gradients in order on themselves, using their own slab
+  // Only the caller's stream forks to the side stream.  Forking `side` (already part of the
+  // capture, forked from the caller's stream) from the input-function stream side2 makes the HIP
+  // runtime crash in hipStreamEndCapture -- observed twice on ROCm 7: round 1 (side2 -> side fork,
+  // side joined into the caller only) and round 2 (the same fork joined back into side2 before
+  // side2 joins the caller, so every fork joined into its forking stream): both segfault at the first
+  // capture while eager execution of the same sequence is correct.  side2's weight gradients
+  // therefore run in order on side2 with their own slab (they are the input-function encoders' and
+  // cross K/V Linears' -- M ~ 10^3 points, microseconds), DESIGN.md "capture fault".
   if (serial || c.s == p->side2) {
     float* slab = c.s == p->side2 ? p->P_("slab_wgrad2") : p->P_("slab_wgrad");
     ProfScope ps(c, "wgrad", group_flops(G));

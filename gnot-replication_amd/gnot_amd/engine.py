@@ -91,9 +91,11 @@ class Engine:
         need = self.lib.gnot_plan_workspace_bytes(self.plan)
         if self.ws is None or self.ws.numel() < need or self.ws.device != device:
             self.ws = None
-            self.ws = torch.empty(need + 256, dtype=torch.uint8, device=device)
-        torch.cuda.current_stream(device).synchronize()
-        _lib.check(self.lib.gnot_plan_bind_workspace(self.plan, self.ws.data_ptr(), self.ws.numel()))
+            # 1/16 headroom: a stream of varying geometries (shuffled meshes) reuses one buffer
+            self.ws = torch.empty(need + need // 16 + 256, dtype=torch.uint8, device=device)
+        # stream-ordered table upload: no host synchronisation on a geometry change
+        s = ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+        _lib.check(self.lib.gnot_plan_bind_workspace_async(self.plan, self.ws.data_ptr(), self.ws.numel(), s))
         if self.comm is not None:
             self.comm.ws = self.ws
         self.geom = geom

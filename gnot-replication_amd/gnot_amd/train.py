@@ -60,9 +60,12 @@ class RelL2Loss(torch.nn.Module):
             B = len(key[0]) - 1
             oh = (ctypes.c_int64 * (B + 1))(*key[0])
             n = _lib.load().gnot_rel_l2_work_floats(oh, B, key[1])
-            self._cache = {key: (torch.tensor(key[0], dtype=torch.int64, device=predictions.device),
-                                 torch.empty(n, dtype=torch.float32, device=predictions.device))}
-        off_dev, work = self._cache[key]
+            # pinned source + non_blocking: a new geometry must not stall the host on the stream
+            # (a pageable copy would); the pinned tensor lives in the cache entry past the copy
+            pinned = torch.tensor(key[0], dtype=torch.int64).pin_memory()
+            self._cache = {key: (pinned.to(predictions.device, non_blocking=True),
+                                 torch.empty(n, dtype=torch.float32, device=predictions.device), pinned)}
+        off_dev, work, _ = self._cache[key]
         return _RelL2.apply(predictions.contiguous().float(), targets.contiguous().float(), off_dev, key[0], work)
 
 

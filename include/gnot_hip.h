@@ -76,9 +76,14 @@ int gnot_plan_bind_params(gnot_plan* plan, const float* const* weights, const fl
 int gnot_plan_set_batch(gnot_plan* plan, int B, const int64_t* x_off, const int64_t* fn_off, int training);
 
 /* Workspace: bytes needed for the current config + batch; bind a device buffer of at least that
- * size (256-byte aligned).  Binding uploads the plan's small device tables (synchronous). */
+ * size (256-byte aligned).  Binding uploads the plan's small device tables: gnot_plan_bind_workspace
+ * synchronously; gnot_plan_bind_workspace_async as one copy from pinned staging ordered on `stream`
+ * (no host wait -- a per-batch geometry change, main.py:41's shuffled variable-size meshes, costs the
+ * host planning (~0.1-0.3 ms) and that copy only).  Either replaces the reference's per-batch
+ * padding/mask set-up, main.py:60-82. */
 size_t gnot_plan_workspace_bytes(const gnot_plan* plan);
 int gnot_plan_bind_workspace(gnot_plan* plan, void* workspace, size_t bytes);
+int gnot_plan_bind_workspace_async(gnot_plan* plan, void* workspace, size_t bytes, void* stream);
 
 /* Parameter-gradient arena inside the workspace: offsets (in floats) of every Linear's weight
  * gradient and bias gradient, grad_off[2*i] / grad_off[2*i+1]. */
