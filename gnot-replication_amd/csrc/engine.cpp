@@ -1401,14 +1401,17 @@ int run_wgrad_side(Ctx& c, const WgradGroup& G, std::initializer_list<const floa
   if (G.jobs.empty()) return GNOT_OK;
   gnot_plan* p = c.p;
   static const bool serial = std::getenv("GNOT_SERIAL_WGRAD") != nullptr;   // diagnostics: no overlap
-  // Only the caller's stream forks to the side stream.  Forking `side` (already part of the
-  // capture, forked from the caller's stream) from the input-function stream side2 makes the HIP
-  // runtime crash in hipStreamEndCapture -- observed twice on ROCm 7: round 1 (side2 -> side fork,
-  // side joined into the caller only) and round 2 (the same fork joined back into side2 before
-  // side2 joins the caller, so every fork joined into its forking stream): both segfault at the first
-  // capture while eager execution of the same sequence is correct.  side2's weight gradients
-  // therefore run in order on side2 with their own slab (they are the input-function encoders' and
-  // cross K/V Linears' -- M ~ 10^3 points, microseconds), DESIGN.md "capture fault".
+  // Only the caller's (capture-origin) stream forks to the side stream.  A fork from the forked
+  // input-function stream side2 segfaults the HIP runtime in hipStreamEndCapture (ROCm 7.2, torch
+  // 2.10), while eager execution of the same sequence is correct.  Four topologies, each run once:
+  //   r1   side2 -> side (side already forked from the origin), side joined into the origin only
+  //   r2a  the same, side's event also joined back into side2 before side2 joins the origin
+  //   r2b  side2 -> side3 (a stream used by nothing else), side3 joined into side2
+  //   r2c  r2b + side3 also joined into the origin
+  // all crash at the first capture; only first-level forks from the origin capture.  side2's weight
+  // gradients therefore run in order on side2 with their own slab: they are the input-function
+  // encoders' and the cross K/V Linears' (M ~ 10^3 points: tens of microseconds).  DESIGN.md
+  // "capture fault".
   if (serial || c.s == p->side2) {
     float* slab = c.s == p->side2 ? p->P_("slab_wgrad2") : p->P_("slab_wgrad");
     ProfScope ps(c, "wgrad", group_flops(G));
