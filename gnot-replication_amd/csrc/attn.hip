@@ -319,6 +319,8 @@ static unsigned seg_split(int H) {
 
 hipError_t launch_attn_apply_fwd(const AttnApplyArgs& a, hipStream_t s) {
   if (a.nchunks <= 0) return hipSuccess;
+  const hipError_t m = launch_attn_apply_mfma(a, false, s);   // attn_mfma.hip where it applies
+  if (m != hipErrorNotSupported) return m;
   GNOT_DH_SWITCH(a.dh, hipLaunchKernelGGL(attn_apply_fwd_kernel<DH>, dim3(a.nchunks, seg_split<DH>(a.H)), dim3(256),
                                           0, s, a));
   return hipGetLastError();
@@ -326,6 +328,8 @@ hipError_t launch_attn_apply_fwd(const AttnApplyArgs& a, hipStream_t s) {
 
 hipError_t launch_attn_apply_bwd(const AttnApplyArgs& a, hipStream_t s) {
   if (a.nchunks <= 0) return hipSuccess;
+  const hipError_t m = launch_attn_apply_mfma(a, true, s);
+  if (m != hipErrorNotSupported) return m;
   GNOT_DH_SWITCH(a.dh, hipLaunchKernelGGL(attn_apply_bwd_kernel<DH>, dim3(a.nchunks, seg_split<DH>(a.H)), dim3(256),
                                           0, s, a));
   return hipGetLastError();

@@ -552,7 +552,8 @@ static void finish_state_group(gnot_plan* p, WgradGroup& G) {
   static const int env_pts = std::getenv("GNOT_STATE_PTS") ? std::atoi(std::getenv("GNOT_STATE_PTS")) : 0;
   if (!G.jobs.empty()) {
     const int d = G.jobs[0].out;
-    G.state_pts = env_pts > 0 ? std::min(env_pts, 8192 / d) : state_pts(d);
+    const int dh = G.jobs[0].state_dh;
+    G.state_pts = env_pts > 0 ? (state_mfma_ok(d, dh) ? env_pts : std::min(env_pts, 8192 / d)) : state_pts(d, dh);
     G.state_nw = 0;
     for (const auto& J : G.jobs)
       if (J.w != nullptr) G.state_nw = d / J.state_dh;
@@ -1375,7 +1376,8 @@ int run_state(Ctx& c, const WgradGroup& G) {
   if (G.jobs.empty()) return GNOT_OK;
   ProfScope ps(c, "state", group_flops(G));
   GNOT_CK(launch_state(G.d_jobs, G.d_wg_prefix, (int)G.jobs.size(), G.total_wgs, G.d_red_prefix,
-                       G.total_red, c.p->P_("slab_state"), G.jobs[0].out, G.state_pts, G.state_nw, c.s));
+                       G.total_red, c.p->P_("slab_state"), G.jobs[0].out, G.jobs[0].state_dh, G.state_pts,
+                       G.state_nw, c.s));
   return GNOT_OK;
 }
 

@@ -1,6 +1,7 @@
 // Internal (C++) launcher interface between the engine and the HIP kernels.
 // The public C-ABI lives in include/gnot_hip.h; nothing here crosses the library boundary.
 #pragma once
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -120,12 +121,18 @@ hipError_t launch_wgrad(const WgradJob* jobs_dev, const int* wg_prefix_dev, int 
 // ------------------------------------------------------------------ attention states (state.hip)
 // Jobs are WgradJobs with state_dh > 0: A = dz/lddz, B = x/ldx, optional w/ldw, out = dW as
 // [H][dh*dh + dh], `splits` partials of state_pts(d) points each at slab + slab_off.
-// points per partial state: the workgroup's A and B rows fill <= 32 KiB of LDS each
-// points per partial-state workgroup (64 at d <= 128, 8192 / d above; measured: 32 and 16 are slower
-// at cfg2); env GNOT_STATE_PTS overrides
-inline int state_pts(int d) { return d <= 128 ? 64 : 8192 / d; }
+// Two kernels: state_mfma (fp32 MFMA, rows straight from HBM, dh = 16/32/64 with H % 4 == 0;
+// env GNOT_STATE_VALU disables it) and the VALU state_partial (LDS-staged rows, any width).
+inline bool state_mfma_ok(int d, int dh) {
+  static const bool valu = std::getenv("GNOT_STATE_VALU") != nullptr;
+  return !valu && (dh == 16 || dh == 32 || dh == 64) && d % dh == 0 && (d / dh) % 4 == 0;
+}
+// points per partial-state workgroup: 256 on MFMA (4 waves per SIMD at 262k points, partials ~6 % of
+// the row bytes); VALU: the workgroup's A and B rows fill <= 32 KiB of LDS each (64 at d <= 128,
+// 8192 / d above; measured: 32 and 16 are slower at cfg2).  env GNOT_STATE_PTS overrides
+inline int state_pts(int d, int dh) { return state_mfma_ok(d, dh) ? 256 : d <= 128 ? 64 : 8192 / d; }
 hipError_t launch_state(const WgradJob* jobs_dev, const int* wg_prefix_dev, int njobs, int total_wgs,
-                        const int* red_prefix_dev, int total_red, float* slab, int d, int pts, int nw,
+                        const int* red_prefix_dev, int total_red, float* slab, int d, int dh, int pts, int nw,
                         hipStream_t s);   // d: row width, pts: points per workgroup, nw: per-point weights (0 or H)
 
 // ------------------------------------------------------------------ attention (attn.hip)
@@ -145,6 +152,8 @@ struct AttnApplyArgs {
 };
 hipError_t launch_attn_apply_fwd(const AttnApplyArgs& a, hipStream_t s);
 hipError_t launch_attn_apply_bwd(const AttnApplyArgs& a, hipStream_t s);
+// fp32-MFMA variants (attn_mfma.hip, dh = 16/32/64); hipErrorNotSupported when not applicable
+hipError_t launch_attn_apply_mfma(const AttnApplyArgs& a, bool bwd, hipStream_t s);
 
 struct AttnKVBwdArgs {
   const float* k; const float* v; long ldkv;   // post-softmax k, v (point-major)

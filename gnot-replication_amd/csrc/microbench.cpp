@@ -228,10 +228,12 @@ int main(int argc, char** argv) {
         ap.du[i] = du + (size_t)i * P * D;
         ap.dden[i] = dden + (size_t)i * P * H;
       }
+      // algorithmic HBM bytes: fwd reads q, writes res; bwd reads q, dres, writes du (per source), dq, dden
+      const double bf = 2.0 * P * D * 4, bb = (3.0 + nsrc) * P * D * 4 + 4.0 * nsrc * P * H;
       t = time_us([&] { CK(launch_attn_apply_fwd(ap, nullptr)); });
-      std::printf("apply_fwd  nsrc=%d P=%d H=%d dh=%d: %8.2f us\n", nsrc, P, H, dh, t);
+      std::printf("apply_fwd  nsrc=%d P=%d H=%d dh=%d: %8.2f us  %6.0f GB/s\n", nsrc, P, H, dh, t, bf / t / 1e3);
       t = time_us([&] { CK(launch_attn_apply_bwd(ap, nullptr)); });
-      std::printf("apply_bwd  nsrc=%d P=%d H=%d dh=%d: %8.2f us\n", nsrc, P, H, dh, t);
+      std::printf("apply_bwd  nsrc=%d P=%d H=%d dh=%d: %8.2f us  %6.0f GB/s\n", nsrc, P, H, dh, t, bb / t / 1e3);
       // contention: wgrad launches queued on s2 while apply_bwd is timed on the null stream
       for (int i = 0; i < 30; ++i) CK(launch_wgrad(djobs, dpre, njobs, wg, dpre + njobs, red, slab, s2));
       t = time_us([&] { CK(launch_attn_apply_bwd(ap, nullptr)); }, 20);

@@ -7,7 +7,7 @@
 // [H][dh*dh + dh] state to a slab and state_reduce sums the partials in a fixed order, so results
 // are bitwise reproducible (no atomics).
 //
-// Each thread owns a 4x4 block of one head's S (and the 4 matching z entries, kept by every
+// VALU form (any head width): each thread owns a 4x4 block of one head's S (and the 4 matching z entries, kept by every
 // block; only j-block 0 stores them).  Arithmetic is plain fp32 FMA on the VALU: H*dh^2 MACs per
 // point (2 Ki at d=128, H=8) against 2*d*4 bytes of rows, so the pass is bound by row traffic and
 // latency, not math.  It replaces a 128x128 MFMA tile of which only the H diagonal dh x dh blocks
@@ -145,6 +145,87 @@ __global__ void __launch_bounds__(kStateThreads) state_partial_kernel(const Wgra
   }
 }
 
+// ---- fp32 MFMA form (dh = 16/32/64, H % 4 == 0): wave w owns heads w*HPW .. w*HPW+HPW-1 of the
+// workgroup's `pts` points; per 4-point k-step one v_mfma_f32_16x16x4_f32 per 16x16 tile of S:
+//   A[i][k] = A_row[p0 + k][h*dh + 16I + i]   (lane (i, g=k) loads one float)
+//   B[k][j] = B_row[p0 + k][h*dh + 16J + j]
+// so every row element is loaded once, straight from HBM into the operand registers (no LDS), and
+// z = sum_p w A_row is a lane-local FMA finished by two shuffles.  Exact fp32 products, fp32 sums,
+// fixed order: deterministic.
+template <int DH, int HPW>
+__global__ void __launch_bounds__(256) state_mfma_kernel(const WgradJob* __restrict__ jobs,
+                                                         const int* __restrict__ prefix, int njobs,
+                                                         float* __restrict__ slab, int pts) {
+  constexpr int NT = DH / 16, U = 8;   // U 4-point steps per batch of loads in flight
+  const int j = find_job_s(prefix, njobs, blockIdx.x);
+  const WgradJob& J = jobs[j];
+  const int split = blockIdx.x - prefix[j];
+  const int H = J.out / DH;
+  const long p0 = (long)split * pts;
+  const long pend = min(p0 + (long)pts, (long)J.P);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, i16 = lane & 15, g = lane >> 4;
+  const bool use_w = J.w != nullptr;
+  const float* __restrict__ Ar = J.dz;
+  const float* __restrict__ Br = J.x;
+  f32x4 acc[HPW][NT][NT];
+  float zp[HPW][NT];
+#pragma unroll
+  for (int kh = 0; kh < HPW; ++kh)
+#pragma unroll
+    for (int I = 0; I < NT; ++I) {
+      zp[kh][I] = 0.f;
+#pragma unroll
+      for (int Jt = 0; Jt < NT; ++Jt) acc[kh][I][Jt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  const int col0 = wave * HPW * DH + i16;
+  for (long pb = p0; pb < pend; pb += 4 * U) {
+    float a[U][HPW][NT], b[U][HPW][NT], w[U][HPW];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long pp = pb + 4 * u + g;
+      const bool valid = pp < pend;
+      const long pr = valid ? pp : p0;
+#pragma unroll
+      for (int kh = 0; kh < HPW; ++kh) {
+#pragma unroll
+        for (int I = 0; I < NT; ++I) {
+          const float av = Ar[pr * J.lddz + col0 + kh * DH + 16 * I];
+          const float bv = Br[pr * J.ldx + col0 + kh * DH + 16 * I];
+          a[u][kh][I] = valid ? av : 0.f;
+          b[u][kh][I] = valid ? bv : 0.f;
+        }
+        w[u][kh] = use_w ? J.w[pr * J.ldw + wave * HPW + kh] : 1.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int kh = 0; kh < HPW; ++kh)
+#pragma unroll
+        for (int I = 0; I < NT; ++I) {
+          zp[kh][I] = fmaf(w[u][kh], a[u][kh][I], zp[kh][I]);
+#pragma unroll
+          for (int Jt = 0; Jt < NT; ++Jt) acc[kh][I][Jt] = mfma4(a[u][kh][I], b[u][kh][Jt], acc[kh][I][Jt]);
+        }
+  }
+  float* S = slab + J.slab_off + (long)split * H * (DH * DH + DH);
+#pragma unroll
+  for (int kh = 0; kh < HPW; ++kh) {
+    float* Sh = S + (wave * HPW + kh) * (DH * DH + DH);
+#pragma unroll
+    for (int I = 0; I < NT; ++I) {
+#pragma unroll
+      for (int Jt = 0; Jt < NT; ++Jt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Sh[(16 * I + 4 * g + r) * DH + 16 * Jt + i16] = acc[kh][I][Jt][r];
+      float z = zp[kh][I];
+      z += __shfl_xor(z, 16, 64);
+      z += __shfl_xor(z, 32, 64);
+      if (g == 0) Sh[DH * DH + 16 * I + i16] = z;
+    }
+  }
+}
+
 // out[e] = sum over splits of the partials: 8 lanes per state element, each summing every 8th
 // split with 4 loads in flight, then a fixed butterfly -> deterministic.
 __global__ void __launch_bounds__(256) state_reduce_kernel(const WgradJob* __restrict__ jobs,
@@ -176,9 +257,23 @@ __global__ void __launch_bounds__(256) state_reduce_kernel(const WgradJob* __res
 }
 
 hipError_t launch_state(const WgradJob* jobs_dev, const int* wg_prefix_dev, int njobs, int total_wgs,
-                        const int* red_prefix_dev, int total_red, float* slab, int d, int pts, int nw,
+                        const int* red_prefix_dev, int total_red, float* slab, int d, int dh, int pts, int nw,
                         hipStream_t s) {
   if (njobs <= 0 || total_wgs <= 0) return hipSuccess;
+  if (state_mfma_ok(d, dh)) {
+    const int hpw = d / dh / 4;
+    const dim3 grid(total_wgs), block(256);
+#define GNOT_STATE_MFMA(DHV, HPWV)                                                                             \
+    if (dh == DHV && hpw == HPWV) {                                                                            \
+      hipLaunchKernelGGL((state_mfma_kernel<DHV, HPWV>), grid, block, 0, s, jobs_dev, wg_prefix_dev, njobs, slab, pts); \
+    } else
+    GNOT_STATE_MFMA(16, 1) GNOT_STATE_MFMA(16, 2) GNOT_STATE_MFMA(16, 4) GNOT_STATE_MFMA(32, 1) GNOT_STATE_MFMA(32, 2)
+    GNOT_STATE_MFMA(32, 4) GNOT_STATE_MFMA(64, 1) GNOT_STATE_MFMA(64, 2) return hipErrorInvalidValue;
+#undef GNOT_STATE_MFMA
+    hipLaunchKernelGGL(state_reduce_kernel, dim3((total_red * 8 + 255) / 256), dim3(256), 0, s, jobs_dev, red_prefix_dev,
+                       njobs, total_red, (const float*)slab);
+    return hipGetLastError();
+  }
   // dynamic LDS, exactly what the workgroup stages: A and B rows (pts * d floats each) + the
   // per-(point, head) weights; the partial-state combine reuses the A/B region (256 x 20 floats)
   const size_t lds = std::max<size_t>((size_t)(2 * pts * d + pts * nw), 256 * 20) * sizeof(float);
