@@ -337,6 +337,8 @@ hipError_t launch_attn_apply_bwd(const AttnApplyArgs& a, hipStream_t s) {
 
 hipError_t launch_attn_kv_bwd(const AttnKVBwdArgs& a, hipStream_t s) {
   if (a.nchunks <= 0) return hipSuccess;
+  const hipError_t m = launch_attn_kv_bwd_mfma(&a, nullptr, 1, a.nchunks, a.H, a.dh, s);
+  if (m != hipErrorNotSupported) return m;
   GNOT_DH_SWITCH(a.dh, hipLaunchKernelGGL(attn_kv_bwd_kernel<DH>, dim3(a.nchunks, seg_split<DH>(a.H)), dim3(256), 0,
                                           s, a));
   return hipGetLastError();
@@ -345,6 +347,9 @@ hipError_t launch_attn_kv_bwd(const AttnKVBwdArgs& a, hipStream_t s) {
 hipError_t launch_attn_kv_bwd_batch(const AttnKVBwdArgs* jobs_dev, int njobs, int maxchunks, int H, int dh,
                                     hipStream_t s) {
   if (njobs <= 0 || maxchunks <= 0) return hipSuccess;
+  // the batched jobs' pitches are 4-aligned by construction (rows of d floats)
+  const hipError_t m = launch_attn_kv_bwd_mfma(nullptr, jobs_dev, njobs, maxchunks, H, dh, s);
+  if (m != hipErrorNotSupported) return m;
   GNOT_DH_SWITCH(dh, hipLaunchKernelGGL(attn_kv_bwd_batch_kernel<DH>, dim3(maxchunks, seg_split<DH>(H), njobs),
                                         dim3(256), 0, s, jobs_dev));
   return hipGetLastError();

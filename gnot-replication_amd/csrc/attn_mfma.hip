@@ -38,11 +38,10 @@ size_t apply_lds_bytes(int ns, int H, bool bwd) {
 
 // stage the images of sample b (all sources, all heads) from the [B][H][DH*DH + DH] states
 template <int DH, bool BWD>
-GNOT_DEV void stage_states(const AttnApplyArgs& a, int b, float4* st, float4* sn, float* zl) {
+GNOT_DEV void stage_states(const float* const* state, int nsrc, int H, int b, float4* st, float4* sn, float* zl) {
   using Gm = ApplyGeo<DH>;
   constexpr int ph = DH * DH + DH;
-  const int H = a.H;
-  const int n4 = a.nsrc * H * Gm::IMG;
+  const int n4 = nsrc * H * Gm::IMG;
   for (int i = threadIdx.x; i < n4; i += blockDim.x) {
     const int lane = i % WAVE;
     int rest = i / WAVE;
@@ -50,7 +49,7 @@ GNOT_DEV void stage_states(const AttnApplyArgs& a, int b, float4* st, float4* sn
     const int J = rest % Gm::NT; rest /= Gm::NT;
     const int h = rest % H;
     const int s = rest / H;
-    const float* S = a.state[s] + ((long)b * H + h) * ph;
+    const float* S = state[s] + ((long)b * H + h) * ph;
     const int j = lane & 15, g = lane >> 4;
     // ST: S[16T + 4g + r][16J + j]  (column walk)
     const float* c0 = S + (16 * T + 4 * g) * DH + 16 * J + j;
@@ -58,9 +57,9 @@ GNOT_DEV void stage_states(const AttnApplyArgs& a, int b, float4* st, float4* sn
     // SN: S[16J + j][16T + 4g + r]  (row segment); J plays the output tile K, T the input tile
     if (BWD) sn[i] = *reinterpret_cast<const float4*>(S + (16 * J + j) * DH + 16 * T + 4 * g);
   }
-  for (int i = threadIdx.x; i < a.nsrc * H * DH; i += blockDim.x) {
+  for (int i = threadIdx.x; i < nsrc * H * DH; i += blockDim.x) {
     const int c = i % DH, hs = i / DH;
-    zl[i] = a.state[hs / H][((long)b * H + hs % H) * ph + DH * DH + c];
+    zl[i] = state[hs / H][((long)b * H + hs % H) * ph + DH * DH + c];
   }
 }
 
@@ -130,7 +129,7 @@ __global__ void __launch_bounds__(256) attn_apply_fwd_mfma_kernel(AttnApplyArgs 
     const int4 ch = a.chunks[c];
     if (ch.x != cur_b) {
       __syncthreads();
-      stage_states<DH, false>(a, ch.x, st, nullptr, zl);
+      stage_states<DH, false>(a.state, a.nsrc, H, ch.x, st, nullptr, zl);
       __syncthreads();
       cur_b = ch.x;
     }
@@ -141,9 +140,16 @@ __global__ void __launch_bounds__(256) attn_apply_fwd_mfma_kernel(AttnApplyArgs 
     const long Nb = a.off[ch.x + 1] - off_b;
     const float* qrow = a.q + (valid ? n : 0) * a.ldq;
     float* rbase = a.res + off_b * (long)H * DH + (n - off_b) * DH;
+    float qn[NT][4];
+    load_tiles<NT>(qn, qrow, valid, g);
     for (int h = 0; h < H; ++h) {
+      // the next head's rows are in flight while this head computes
       float q[NT][4];
-      load_tiles<NT>(q, qrow + h * DH, valid, g);
+#pragma unroll
+      for (int T = 0; T < NT; ++T)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) q[T][r] = qn[T][r];
+      if (h + 1 < H) load_tiles<NT>(qn, qrow + (h + 1) * DH, valid, g);
       float o[NT][4];
 #pragma unroll
       for (int T = 0; T < NT; ++T)
@@ -190,7 +196,7 @@ __global__ void __launch_bounds__(256) attn_apply_bwd_mfma_kernel(AttnApplyArgs 
     const int4 ch = a.chunks[c];
     if (ch.x != cur_b) {
       __syncthreads();
-      stage_states<DH, true>(a, ch.x, st, sn, zl);
+      stage_states<DH, true>(a.state, a.nsrc, H, ch.x, st, sn, zl);
       __syncthreads();
       cur_b = ch.x;
     }
@@ -202,10 +208,19 @@ __global__ void __launch_bounds__(256) attn_apply_bwd_mfma_kernel(AttnApplyArgs 
     const long Nb = a.off[ch.x + 1] - off_b;
     const float* qrow = a.q + nv * a.ldq;
     const float* dbase = a.dres + off_b * (long)H * DH + (n - off_b) * DH;
+    float qn[NT][4], dn[NT][4];
+    load_tiles<NT>(qn, qrow, valid, g);
+    load_tiles<NT>(dn, dbase, valid, g);
     for (int h = 0; h < H; ++h) {
       float q[NT][4], dq[NT][4], dO[NT][4];
-      load_tiles<NT>(q, qrow + h * DH, valid, g);
-      load_tiles<NT>(dq, dbase + (long)h * Nb * DH, valid, g);
+#pragma unroll
+      for (int T = 0; T < NT; ++T)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { q[T][r] = qn[T][r]; dq[T][r] = dn[T][r]; }
+      if (h + 1 < H) {
+        load_tiles<NT>(qn, qrow + (h + 1) * DH, valid, g);
+        load_tiles<NT>(dn, dbase + (long)(h + 1) * Nb * DH, valid, g);
+      }
 #pragma unroll
       for (int T = 0; T < NT; ++T)
 #pragma unroll
@@ -254,6 +269,91 @@ __global__ void __launch_bounds__(256) attn_apply_bwd_mfma_kernel(AttnApplyArgs 
   }
 }
 
+// ---------------------------------------------------------------- K/V backward
+// dv = k dS (the ST image of dS), dk = dz + v dS^T (the SN image), then the feature-softmax backward
+// of k: dk_pre = k * (dk - k . dk).  One job = (k, v, dS) of one attention call; the batched form
+// runs every (block, input function) job of the cross attention in one launch (job = blockIdx.z).
+template <int DH>
+GNOT_DEV void kv_bwd_mfma_body(const AttnKVBwdArgs& a, int cpw, int bx) {
+  using Gm = ApplyGeo<DH>;
+  constexpr int NT = Gm::NT;
+  extern __shared__ __attribute__((aligned(16))) float4 alds[];
+  const int H = a.H;
+  float4* st = alds;
+  float4* sn = alds + (size_t)H * Gm::IMG;
+  float* zl = reinterpret_cast<float*>(alds + (size_t)2 * H * Gm::IMG);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const float* const states[1] = {a.dstate};
+  int cur_b = -1;
+  for (int i = 0; i < cpw; ++i) {
+    const int c = bx * cpw + i;
+    if (c >= a.nchunks) break;
+    const int4 ch = a.chunks[c];
+    if (ch.x != cur_b) {
+      __syncthreads();
+      stage_states<DH, true>(states, 1, H, ch.x, st, sn, zl);
+      __syncthreads();
+      cur_b = ch.x;
+    }
+    const int pl = wave * 16 + (lane & 15);
+    const bool valid = pl < ch.z;
+    const long n = ch.y + pl;
+    const long nv = valid ? n : 0;
+    float kn[NT][4], vn[NT][4];
+    load_tiles<NT>(kn, a.k + nv * a.ldkv, valid, g);
+    load_tiles<NT>(vn, a.v + nv * a.ldkv, valid, g);
+    for (int h = 0; h < H; ++h) {
+      float k[NT][4], v[NT][4];
+#pragma unroll
+      for (int T = 0; T < NT; ++T)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { k[T][r] = kn[T][r]; v[T][r] = vn[T][r]; }
+      if (h + 1 < H) {
+        load_tiles<NT>(kn, a.k + nv * a.ldkv + (h + 1) * DH, valid, g);
+        load_tiles<NT>(vn, a.v + nv * a.ldkv + (h + 1) * DH, valid, g);
+      }
+      f32x4 dv[NT], dk[NT];
+      img_mm<NT>(st + (size_t)h * Gm::IMG, k, dv, lane);
+      img_mm<NT>(sn + (size_t)h * Gm::IMG, v, dk, lane);
+      const float* zh = zl + h * DH;
+      float kdk = 0.f;
+      float dko[NT][4], dvo[NT][4];
+#pragma unroll
+      for (int T = 0; T < NT; ++T) {
+        const float4 z = *reinterpret_cast<const float4*>(zh + 16 * T + 4 * g);
+        const float zr[4] = {z.x, z.y, z.z, z.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          dko[T][r] = zr[r] + dk[T][r];
+          dvo[T][r] = dv[T][r];
+          kdk = fmaf(k[T][r], dko[T][r], kdk);
+        }
+      }
+      kdk = point_sum(kdk);
+#pragma unroll
+      for (int T = 0; T < NT; ++T)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dko[T][r] = k[T][r] * (dko[T][r] - kdk);
+      if (valid) {
+        store_tiles<NT>(a.dk + n * a.lddkv + h * DH, dko, g);
+        store_tiles<NT>(a.dv + n * a.lddkv + h * DH, dvo, g);
+      }
+    }
+  }
+}
+
+template <int DH>
+__global__ void __launch_bounds__(256) attn_kv_bwd_mfma_kernel(AttnKVBwdArgs a, int cpw) {
+  kv_bwd_mfma_body<DH>(a, cpw, blockIdx.x);
+}
+
+template <int DH>
+__global__ void __launch_bounds__(256) attn_kv_bwd_batch_mfma_kernel(const AttnKVBwdArgs* __restrict__ jobs, int cpw) {
+  const AttnKVBwdArgs a = jobs[blockIdx.z];
+  if ((int)blockIdx.x * cpw >= a.nchunks) return;
+  kv_bwd_mfma_body<DH>(a, cpw, blockIdx.x);
+}
+
 namespace {
 constexpr size_t kApplyLdsMax = 160 * 1024;
 
@@ -284,6 +384,37 @@ hipError_t launch_attn_apply_mfma(const AttnApplyArgs& a, bool bwd, hipStream_t 
     case 16: if (mfma_ok<16>(a, bwd)) return bwd ? launch_mfma<16, true>(a, s) : launch_mfma<16, false>(a, s); break;
     case 32: if (mfma_ok<32>(a, bwd)) return bwd ? launch_mfma<32, true>(a, s) : launch_mfma<32, false>(a, s); break;
     case 64: if (mfma_ok<64>(a, bwd)) return bwd ? launch_mfma<64, true>(a, s) : launch_mfma<64, false>(a, s); break;
+    default: break;
+  }
+  return hipErrorNotSupported;
+}
+
+namespace {
+template <int DH>
+hipError_t launch_kv(const AttnKVBwdArgs* a, const AttnKVBwdArgs* jobs_dev, int njobs, int maxchunks, int H,
+                     hipStream_t s) {
+  const size_t lds = apply_lds_bytes<DH>(1, H, true);
+  const void* f = a ? reinterpret_cast<const void*>(attn_kv_bwd_mfma_kernel<DH>)
+                    : reinterpret_cast<const void*>(attn_kv_bwd_batch_mfma_kernel<DH>);
+  if (lds > 64 * 1024) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  const int nch = a ? a->nchunks : maxchunks;
+  const dim3 grid((nch + kApplyCpw - 1) / kApplyCpw, 1, a ? 1 : njobs), block(256);
+  if (a) hipLaunchKernelGGL(attn_kv_bwd_mfma_kernel<DH>, grid, block, lds, s, *a, kApplyCpw);
+  else hipLaunchKernelGGL(attn_kv_bwd_batch_mfma_kernel<DH>, grid, block, lds, s, jobs_dev, kApplyCpw);
+  return hipGetLastError();
+}
+}  // namespace
+
+// K/V backward on MFMA: `a` for one job, or (jobs_dev, njobs, maxchunks) for the batched form;
+// hipErrorNotSupported when the head width / LDS size has no MFMA variant
+hipError_t launch_attn_kv_bwd_mfma(const AttnKVBwdArgs* a, const AttnKVBwdArgs* jobs_dev, int njobs, int maxchunks,
+                                   int H, int dh, hipStream_t s) {
+  static const bool valu = std::getenv("GNOT_APPLY_VALU") != nullptr;
+  if (valu || (a && ((a->ldkv & 3) || (a->lddkv & 3)))) return hipErrorNotSupported;
+  switch (dh) {
+    case 16: if (apply_lds_bytes<16>(1, H, true) <= kApplyLdsMax) return launch_kv<16>(a, jobs_dev, njobs, maxchunks, H, s); break;
+    case 32: if (apply_lds_bytes<32>(1, H, true) <= kApplyLdsMax) return launch_kv<32>(a, jobs_dev, njobs, maxchunks, H, s); break;
+    case 64: if (apply_lds_bytes<64>(1, H, true) <= kApplyLdsMax) return launch_kv<64>(a, jobs_dev, njobs, maxchunks, H, s); break;
     default: break;
   }
   return hipErrorNotSupported;

@@ -166,6 +166,10 @@ hipError_t launch_attn_kv_bwd(const AttnKVBwdArgs& a, hipStream_t s);
 // independent K/V backward jobs (every block x input function) in one launch, job = grid.y
 hipError_t launch_attn_kv_bwd_batch(const AttnKVBwdArgs* jobs_dev, int njobs, int maxchunks, int H, int dh,
                                     hipStream_t s);
+// fp32-MFMA K/V backward (attn_mfma.hip): one job (a) or the batched jobs; hipErrorNotSupported
+// when not applicable
+hipError_t launch_attn_kv_bwd_mfma(const AttnKVBwdArgs* a, const AttnKVBwdArgs* jobs_dev, int njobs, int maxchunks,
+                                   int H, int dh, hipStream_t s);
 
 // ------------------------------------------------------------------ small elementwise (misc.hip)
 hipError_t launch_concat_theta(const float* x, long ldx, int in_dim, const float* theta, int th_dim,

@@ -234,6 +234,13 @@ int main(int argc, char** argv) {
       std::printf("apply_fwd  nsrc=%d P=%d H=%d dh=%d: %8.2f us  %6.0f GB/s\n", nsrc, P, H, dh, t, bf / t / 1e3);
       t = time_us([&] { CK(launch_attn_apply_bwd(ap, nullptr)); });
       std::printf("apply_bwd  nsrc=%d P=%d H=%d dh=%d: %8.2f us  %6.0f GB/s\n", nsrc, P, H, dh, t, bb / t / 1e3);
+      if (nsrc == 1) {   // K/V backward of the self attention (k, v = the 2nd/3rd thirds of the qkv rows)
+        AttnKVBwdArgs kb{};
+        kb.k = q + D; kb.v = q + 2 * D; kb.ldkv = 3 * D; kb.dstate = st; kb.chunks = dch; kb.nchunks = (int)ch.size();
+        kb.H = H; kb.dh = dh; kb.dk = dq + D; kb.dv = dq + 2 * D; kb.lddkv = 3 * D;
+        t = time_us([&] { CK(launch_attn_kv_bwd(kb, nullptr)); });
+        std::printf("kv_bwd     P=%d H=%d dh=%d: %8.2f us  %6.0f GB/s\n", P, H, dh, t, 4.0 * P * D * 4 / t / 1e3);
+      }
       // contention: wgrad launches queued on s2 while apply_bwd is timed on the null stream
       for (int i = 0; i < 30; ++i) CK(launch_wgrad(djobs, dpre, njobs, wg, dpre + njobs, red, slab, s2));
       t = time_us([&] { CK(launch_attn_apply_bwd(ap, nullptr)); }, 20);
