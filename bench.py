@@ -138,7 +138,8 @@ def make_rank_batch(w, rank, world, device):
         lo, hi = par.shard_range(w["N"], rank, world)
         to = lambda t: t.to(device)
         return dict(x=to(x[lo:hi]), x_off=[0, hi - lo], theta=to(theta), fns=[to(f) for f in fns], fn_offs=fn_offs,
-                    y=to(y[lo:hi]), seg=to(seg[lo:hi]), B=1, norm=1, n_global=[w["N"]], step_points=w["N"],
+                    y=to(y[lo:hi]), seg=to(seg[lo:hi]), B=1, norm=1, n_global=[w["N"]] if world > 1 else None,
+                    step_points=w["N"],
                     mesh_points=f"{w['N']:,} ({hi - lo:,} on this GPU)", meshes=1)
     x, x_off, theta, fns, fn_offs, y, seg = make_batch(w, 100 + rank, device)
     return dict(x=x, x_off=x_off, theta=theta, fns=fns, fn_offs=fn_offs, y=y, seg=seg, B=w["B"],
@@ -237,6 +238,9 @@ def main():
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--torch-adamw", action="store_true", help="torch's fused AdamW instead of the native one")
     ap.add_argument("--breakdown", action="store_true", help="print per-kernel-class device time to stderr")
+    ap.add_argument("--recompute", choices=["auto", "on", "off"], default="auto",
+                    help="MoE activation recompute (GNOT.set_moe_recompute); auto: on when the plain workspace "
+                         "would not fit the GPU (configs[3]'s 1M-point mesh on one GPU)")
     ap.add_argument("--vary-geometry", action="store_true",
                     help="variable-mesh workloads: a new mesh order (hence new packed offsets) every step, as "
                          "main.py:41's shuffled DataLoader does; eager launches")
@@ -287,6 +291,22 @@ def main():
     x, x_off, theta, fns, fn_offs, y, seg, B = (D[k] for k in ("x", "x_off", "theta", "fns", "fn_offs", "y", "seg", "B"))
     eng = model.engine()
     eng.param_grads = bool(args.torch_adamw)      # the native AdamW reads the gradient arena directly
+    recompute = args.recompute == "on"
+    if args.recompute == "auto":
+        # the plan's training workspace for this rank's geometry vs ~90 % of the free device memory
+        import ctypes
+        from gnot_amd import _lib
+        lib = _lib.load()
+        nx = D["x_off"]
+        B_ = len(nx) - 1
+        flat = [v for o in D["fn_offs"] for v in o]
+        _lib.check(lib.gnot_plan_set_batch(eng.plan, B_, (ctypes.c_int64 * (B_ + 1))(*nx),
+                                           (ctypes.c_int64 * max(1, len(flat)))(*flat) if flat else None, 1))
+        need = lib.gnot_plan_workspace_bytes(eng.plan)
+        free, _ = torch.cuda.mem_get_info(device)
+        recompute = need > 0.9 * free
+        eng.geom = None
+    model.set_moe_recompute(recompute)
     batches = None
     if args.vary_geometry:
         if not w.get("variable"):
@@ -433,6 +453,7 @@ def main():
                    "heads": m["n_head"], "blocks": m["n_attn_layers"], "mlp_layers": m["n_mlp_num_layers"],
                    "input_functions": m["n_input_functions"],
                    "geometry": "new mesh order every step (--vary-geometry)" if batches is not None else "fixed",
+                   "moe_recompute": recompute,
                    "parallelism": (f"point-shard{world}" if shard else f"sample-dp{world}") if world > 1 else "single",
                    "step": "pack+fwd+RelL2+bwd+AdamW (native loss, " + ("torch fused AdamW" if args.torch_adamw else "native flat AdamW") + ")" + (" (hipGraph replay)" if use_graph else " (eager)")},
         "roofline": {

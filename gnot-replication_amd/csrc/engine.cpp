@@ -175,6 +175,13 @@ struct gnot_plan {
   gnot_comm comm{};
   std::vector<long> nglob;                 // [B] global points per sample (sharded batches)
   bool sharded = false;                    // world > 1 for the current batch
+  // MoE activation recompute (gnot_plan_set_moe_recompute): training keeps only each MoE call's
+  // input; the backward re-runs that call's expert forward into ONE shared save buffer ("mrsave")
+  // just before its chain backward -- E*NL*P*D floats once instead of per MoE call
+  bool moe_recompute = false;
+  std::string msave(int l, bool m1) const {
+    return moe_recompute ? std::string("mrsave") : "b" + std::to_string(l) + (m1 ? ".m1save" : ".m2save");
+  }
   std::vector<CopySeg> xsend, xrecv;       // scramble all-to-all: hm -> send buffer, recv buffer -> tokens
   std::vector<int> xsend_prefix, xrecv_prefix;   // float4 prefix sums for the copy kernel
   std::vector<int64_t> xsend_counts, xrecv_counts;
@@ -722,8 +729,8 @@ static void build_groups(gnot_plan* p) {
     const std::string s = "b" + std::to_string(l) + ".";
     std::vector<int> f1, f2;
     for (int e = 0; e < E; ++e) { f1.push_back(p->lin_f1(l, e, 0)); f2.push_back(p->lin_f2(l, e, 0)); }
-    chain_group(p->wg_m1[l], p->k_m1(l), f1, P, p->P_(s + "a"), D, p->P_(s + "m1save"));
-    chain_group(p->wg_m2[l], p->k_m2(l), f2, P, p->P_(s + "bb"), D, p->P_(s + "m2save"));
+    chain_group(p->wg_m1[l], p->k_m1(l), f1, P, p->P_(s + "a"), D, p->P_(p->msave(l, true)));
+    chain_group(p->wg_m2[l], p->k_m2(l), f2, P, p->P_(s + "bb"), D, p->P_(p->msave(l, false)));
     {
       float* dsum = p->P_(p->dsum_buf(false));
       float* dqkv = p->P_(p->dqkv_buf(false));
@@ -925,6 +932,16 @@ extern "C" int gnot_plan_set_shard(gnot_plan* p, int rank, int world, int B, con
   return GNOT_OK;
 }
 
+extern "C" int gnot_plan_set_moe_recompute(gnot_plan* p, int on) {
+  if (!p) return fail(GNOT_E_INVALID, "null plan");
+  if (p->moe_recompute != (on != 0)) {
+    p->moe_recompute = on != 0;
+    p->batch_set = false;          // the workspace layout changes: set_batch + bind again
+    p->ws_bound = false;
+  }
+  return GNOT_OK;
+}
+
 extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, const int64_t* fn_off,
                                    int training) {
   if (!p || B <= 0 || !x_off) return fail(GNOT_E_INVALID, "bad batch arguments");
@@ -1016,16 +1033,17 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
     for (int i = 0; i < KI; ++i) C.add(s + "cstate" + std::to_string(i), p->B * per_state, per_state);
     C.add(s + "cres", P * D, D);
     C.add(s + "a", P * D, D);
-    if (tr) C.add(s + "m1save", E * NL * P * D, D);
+    if (tr && !p->moe_recompute) C.add(s + "m1save", E * NL * P * D, D);
     C.add(s + "query1", P * D, D);
     C.add(s + "sq", P * 3 * D, 3 * D);
     C.add(s + "sstate", p->B * per_state, per_state);
     C.add(s + "sres", P * D, D);
     C.add(s + "bb", P * D, D);
-    if (tr) C.add(s + "m2save", E * NL * P * D, D);
+    if (tr && !p->moe_recompute) C.add(s + "m2save", E * NL * P * D, D);
     C.add(s + "query2", P * D, D);
   }
   C.add("stage", E * P * D, D);
+  if (tr && p->moe_recompute && p->L > 0) C.add("mrsave", E * NL * P * D, D);
   if (p->sharded) {                          // scramble exchange scratch: head-major rows / packed peers
     C.add("xa", P * D, D);
     C.add("xb", P * D, D);
@@ -1646,7 +1664,9 @@ extern "C" int gnot_forward(gnot_plan* p, const float* x, const float* theta, co
       ChainArgs a = chain_args(p, p->ch_m1[l], P);
       a.X = p->P_(s + "a"); a.ldx = D; a.Y = p->P_("stage"); a.ldy = D; a.y_chain_stride = P * D;
       a.scores = p->P_("scores"); a.ldsc = (int)p->bufs["scores"].ld; a.mode = CH_MOE;
-      if (tr) { a.save = p->P_(s + "m1save"); a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D; }
+      if (tr && !p->moe_recompute) {
+        a.save = p->P_(s + "m1save"); a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D;
+      }
       {
         ProfScope ps(c, "moe_fwd", 2.0 * E * P * NL * (double)D * D);
         GNOT_CK(launch_chain_fwd(a, c.s));
@@ -1658,7 +1678,9 @@ extern "C" int gnot_forward(gnot_plan* p, const float* x, const float* theta, co
       ChainArgs a = chain_args(p, p->ch_m2[l], P);
       a.X = p->P_(s + "bb"); a.ldx = D; a.Y = p->P_("stage"); a.ldy = D; a.y_chain_stride = P * D;
       a.scores = p->P_("scores"); a.ldsc = (int)p->bufs["scores"].ld; a.mode = CH_MOE;
-      if (tr) { a.save = p->P_(s + "m2save"); a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D; }
+      if (tr && !p->moe_recompute) {
+        a.save = p->P_(s + "m2save"); a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D;
+      }
       {
         ProfScope ps(c, "moe_fwd", 2.0 * E * P * NL * (double)D * D);
         GNOT_CK(launch_chain_fwd(a, c.s));
@@ -1700,6 +1722,9 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
       ProfScope ps(cc, prof, 2.0 * a.nchains * rows * NL * (double)D * D);
       GNOT_CK(launch_chain_bwd(a, cc.s));
     }
+    // the weight gradients read the saved pre-activations too: a recomputed (shared) save buffer
+    // must not be overwritten by the next MoE's recompute before they finish
+    if (p->moe_recompute && a.mode == CH_MOE) return run_wgrad_side(cc, G, {dz, a.save});
     return run_wgrad_side(cc, G, {dz});
   };
   auto chain_bwd = [&](ChainArgs& a, int kcall, long rows, const WgradGroup& G, const char* prof) -> int {
@@ -1718,10 +1743,21 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
     // ffn2 experts: query2 = query1 + sum_e s_e ffn2_e(bb)   (model.py:134-137)
     for (int m = 2; m >= 1; --m) {
       const bool m1 = (m == 1);
+      if (p->moe_recompute) {
+        // re-run this call's expert forward (inputs kept: "a" / "bb") into the shared save buffer
+        float* mr = p->P_("mrsave");
+        GNOT_RUN(guard_write(c, mr));
+        ChainArgs f = chain_args(p, m1 ? p->ch_m1[l] : p->ch_m2[l], P);
+        f.X = p->P_(s + (m1 ? "a" : "bb")); f.ldx = D; f.Y = stage; f.ldy = D; f.y_chain_stride = P * D;
+        f.scores = p->P_("scores"); f.ldsc = (int)p->bufs["scores"].ld; f.mode = CH_MOE;
+        f.save = mr; f.save_layer_stride = P * D; f.save_chain_stride = NL * P * D;
+        ProfScope ps(c, "moe_recompute", 2.0 * E * P * NL * (double)D * D);
+        GNOT_CK(launch_chain_fwd(f, c.s));
+      }
       ChainArgs a = chain_args(p, m1 ? p->ch_m1[l] : p->ch_m2[l], P);
       a.dY = dquery; a.lddy = D; a.mode = CH_MOE;
       a.scores = p->P_("scores"); a.ldsc = (int)p->bufs["scores"].ld; a.dscore = p->P_("dscore");
-      a.save = p->P_(s + (m1 ? "m1save" : "m2save")); a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D;
+      a.save = p->P_(p->msave(l, m1)); a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D;
       a.dX = stage; a.lddx = D; a.dx_chain_stride = P * D;
       GNOT_RUN(chain_bwd(a, m1 ? p->k_m1(l) : p->k_m2(l), P, m1 ? p->wg_m1[l] : p->wg_m2[l], "moe_bwd"));
       float* dsum = p->P_(p->dsum_buf(m1));

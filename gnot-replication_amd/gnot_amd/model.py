@@ -136,6 +136,7 @@ class GNOT(nn.Module):
                          n_input_functions=n_input_functions)
         self._engine = None
         self._comm = None          # parallel.PointShardComm (set_point_shard); survives engine rebuilds
+        self._moe_recompute = False
 
     # canonical Linear order == named_parameters() order of the reference module
     def linears(self):
@@ -150,7 +151,16 @@ class GNOT(nn.Module):
         if self._engine is None:
             self._engine = Engine(self._cfg, self.linears())
             self._engine.comm = self._comm
+            self._engine.moe_recompute = self._moe_recompute
         return self._engine
+
+    def set_moe_recompute(self, on=True):
+        """Memory option (no reference counterpart; torch.utils.checkpoint is the analogue): keep only
+        each MoE call's input in training and re-run its expert forward (model.py:128/134) inside the
+        backward, so the experts' saved pre-activations exist once instead of once per MoE call.
+        Same results; one more MoE forward per call."""
+        self._moe_recompute = bool(on)
+        self.engine().moe_recompute = self._moe_recompute
 
     def _apply(self, fn, *args, **kwargs):
         # moving / casting the module invalidates the bound parameter pointers

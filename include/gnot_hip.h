@@ -75,6 +75,14 @@ int gnot_plan_bind_params(gnot_plan* plan, const float* const* weights, const fl
  * training != 0 keeps the activations the backward needs. */
 int gnot_plan_set_batch(gnot_plan* plan, int B, const int64_t* x_off, const int64_t* fn_off, int training);
 
+/* MoE activation recompute (off by default): training keeps only each MoE call's input and the
+ * backward re-runs that call's expert forward (model.py:128/134's ffn1/ffn2 experts) into one shared
+ * save buffer just before its chain backward -- the E*nl*P*d saved pre-activations exist once instead
+ * of once per MoE call (2 per block), at the cost of one more MoE forward per call.  Changing it
+ * invalidates the batch: call gnot_plan_set_batch (and bind) again.  No reference counterpart (a
+ * memory option of this library; torch.utils.checkpoint is the analogue). */
+int gnot_plan_set_moe_recompute(gnot_plan* plan, int on);
+
 /* Workspace: bytes needed for the current config + batch; bind a device buffer of at least that
  * size (256-byte aligned).  Binding uploads the plan's small device tables: gnot_plan_bind_workspace
  * synchronously; gnot_plan_bind_workspace_async as one copy from pinned staging ordered on `stream`

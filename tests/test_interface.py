@@ -122,3 +122,33 @@ def test_missing_input_functions_raises_like_reference():
     m = GNOT(2, 1, 3, 1, 1, 32, 2, 32, 32, 2, 4, 1)
     with pytest.raises(NotImplementedError):
         m(torch.rand(1, 10, 2), torch.rand(1, 1))
+
+
+def test_moe_recompute_shrinks_training_workspace():
+    """gnot_plan_set_moe_recompute: the per-MoE-call saves (E*nl*P*d each, 2 per block) become one
+    shared buffer; it invalidates the batch (set_batch must run again)."""
+    from gnot_amd import _lib
+    lib = _lib.load()
+    cfg = _lib.GnotConfig(input_dim=3, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=4,
+                          n_attn_hidden_dim=64, n_mlp_num_layers=4, n_mlp_hidden_dim=64, n_input_hidden_dim=64,
+                          n_expert=8, n_head=4, n_input_functions=1)
+    plan = ctypes.c_void_p()
+    _lib.check(lib.gnot_plan_create(ctypes.byref(cfg), ctypes.byref(plan)))
+    try:
+        P, M, E, NL, L, d = 4096, 100, 8, 5, 4, 64
+        xo, fo = (ctypes.c_int64 * 2)(0, P), (ctypes.c_int64 * 2)(0, M)
+        _lib.check(lib.gnot_plan_set_batch(plan, 1, xo, fo, 1))
+        plain = lib.gnot_plan_workspace_bytes(plan)
+        _lib.check(lib.gnot_plan_set_moe_recompute(plan, 1))
+        assert lib.gnot_plan_workspace_bytes(plan) == 0          # batch invalidated
+        _lib.check(lib.gnot_plan_set_batch(plan, 1, xo, fo, 1))
+        rc = lib.gnot_plan_workspace_bytes(plan)
+        saves = E * NL * P * d * 4
+        assert plain - rc >= (2 * L - 1) * saves * 0.99, (plain, rc)
+        _lib.check(lib.gnot_plan_set_batch(plan, 1, xo, fo, 0))  # inference: no saves either way
+        inf_rc = lib.gnot_plan_workspace_bytes(plan)
+        _lib.check(lib.gnot_plan_set_moe_recompute(plan, 0))
+        _lib.check(lib.gnot_plan_set_batch(plan, 1, xo, fo, 0))
+        assert lib.gnot_plan_workspace_bytes(plan) == inf_rc
+    finally:
+        lib.gnot_plan_destroy(plan)
