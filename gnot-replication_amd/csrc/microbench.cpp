@@ -77,7 +77,9 @@ int main(int argc, char** argv) {
   a.scores = scores; a.ldsc = 16; a.mode = CH_MOE;
   a.save = save; a.save_layer_stride = (long)P * D; a.save_chain_stride = (long)NL * P * D;
   const double fl = 2.0 * E * P * NL * (double)D * D;
-  double t = time_us([&] { CK(launch_chain_fwd(a, nullptr)); });
+  double t = time_us([&] { CK(launch_moe_combine(X, Y, (long)P * D, E, dX, (long)P * D, nullptr)); });
+  std::printf("moe_combine E=%d P=%d D=%d: %8.2f us  %6.0f GB/s\n", E, P, D, t, (E + 2.0) * P * D * 4 / t / 1e3);
+  t = time_us([&] { CK(launch_chain_fwd(a, nullptr)); });
   std::printf("chain_fwd  MoE E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
   ChainArgs bw = a;
   bw.dY = X; bw.lddy = D; bw.dscore = dscore; bw.dz = dz; bw.dz_layer_stride = (long)P * D;
