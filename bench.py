@@ -61,36 +61,36 @@ WORKLOADS = {
                             n_input_hidden_dim=128, n_expert=4, n_head=8, n_input_functions=2),
                  N=10000, M=805, B=1,
                  desc="configs[1]: GNOT 4-layer, 4-expert, d=128, 8 heads, 2 input functions, "
-                      "2-D irregular mesh of {N} points/sample (805 points per input function), fp32 fwd+bwd"),
-    # BASELINE.json configs[2]: synthetic 3-D mesh, 256k points, d=256, 8 experts (the reference
-    # config is bf16; this path computes the reference's fp32)
+                      "2-D irregular mesh of {N} points/sample (805 points per input function), {dtype} fwd+bwd"),
+    # BASELINE.json configs[2]: synthetic 3-D mesh, 256k points, d=256, 8 experts (the reference config
+    # names bf16 training: --dtype bf16; the default computes the reference's fp32, bf16x6-exact)
     "cfg3": dict(model=dict(input_dim=3, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=4,
                             n_attn_hidden_dim=256, n_mlp_num_layers=4, n_mlp_hidden_dim=256,
                             n_input_hidden_dim=256, n_expert=8, n_head=8, n_input_functions=1),
                  N=262144, M=805, B=1, shard_weak=True,
                  desc="configs[2]: synthetic 3-D mesh of {N} points, d=256, 8 experts, 8 heads, "
-                      "1 input function (805 points), fp32 fwd+bwd"),
+                      "1 input function (805 points), {dtype} fwd+bwd"),
     # BASELINE.json configs[3]: ONE 1M-point mesh point-sharded over the ranks (strong scaling)
     "cfg4": dict(model=dict(input_dim=3, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=4,
                             n_attn_hidden_dim=256, n_mlp_num_layers=4, n_mlp_hidden_dim=256,
                             n_input_hidden_dim=256, n_expert=8, n_head=8, n_input_functions=1),
                  N=1048576, M=805, B=1, shard=True,
                  desc="configs[3]: synthetic 3-D mesh of {N} points point-sharded over the GPUs "
-                      "(state all-reduce + scramble all-to-all over RCCL), d=256, 8 experts, fp32 fwd+bwd"),
+                      "(state all-reduce + scramble all-to-all over RCCL), d=256, 8 experts, {dtype} fwd+bwd"),
     # BASELINE.json configs[4]: 64 variable meshes (1k-50k points, packed), sample-DP with LPT balancing
     "cfg5": dict(model=dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=4,
                             n_attn_hidden_dim=256, n_mlp_num_layers=4, n_mlp_hidden_dim=256,
                             n_input_hidden_dim=256, n_expert=3, n_head=8, n_input_functions=1),
                  N=0, M=805, B=64, variable=(1000, 50000),
                  desc="configs[4]: {B} meshes of U{{1k..50k}} points (seeded), packed offsets, sample-DP over the "
-                      "GPUs with longest-processing-time balancing, main.py widths, fp32 fwd+bwd"),
+                      "GPUs with longest-processing-time balancing, main.py widths, {dtype} fwd+bwd"),
     # BASELINE.json configs[0] (main.py defaults, ~1-4k points/sample, batch 4)
     "cfg1": dict(model=dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=4,
                             n_attn_hidden_dim=256, n_mlp_num_layers=4, n_mlp_hidden_dim=256,
                             n_input_hidden_dim=256, n_expert=3, n_head=8, n_input_functions=1),
                  N=4096, M=805, B=4,
                  desc="configs[0]: main.py defaults d=256, 3 experts, 8 heads, 1 input function, "
-                      "batch {B} x {N} points, fp32 fwd+bwd"),
+                      "batch {B} x {N} points, {dtype} fwd+bwd"),
 }
 
 
@@ -238,6 +238,10 @@ def main():
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
     ap.add_argument("--torch-adamw", action="store_true", help="torch's fused AdamW instead of the native one")
     ap.add_argument("--breakdown", action="store_true", help="print per-kernel-class device time to stderr")
+    ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32",
+                    help="fp32: the reference's arithmetic (bf16x6-exact MFMA); bf16: configs[2]'s bf16 training "
+                         "(one RNE bf16 operand per MFMA in the d=256 chains / projections / weight gradients, "
+                         "fp32 accumulation and storage; north_star's 1e-2 bar, tests/test_gpu_bf16.py)")
     ap.add_argument("--recompute", choices=["auto", "on", "off"], default="auto",
                     help="MoE activation recompute (GNOT.set_moe_recompute); auto: on when the plain workspace "
                          "would not fit the GPU (configs[3]'s 1M-point mesh on one GPU)")
@@ -307,6 +311,7 @@ def main():
         recompute = need > 0.9 * free
         eng.geom = None
     model.set_moe_recompute(recompute)
+    model.set_precision(args.dtype)
     batches = None
     if args.vary_geometry:
         if not w.get("variable"):
@@ -444,10 +449,10 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if (w.get("shard") and world > 1) else "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": args.dtype,
         "data": "synthetic: coords/theta/input-function rows U[0,1], targets N(0,1), seeded per rank; "
                 "random-init weights (torch.manual_seed)",
-        "config": {"workload": w["desc"].format(N=D["mesh_points"], B=D["meshes"]),
+        "config": {"workload": w["desc"].format(N=D["mesh_points"], B=D["meshes"], dtype=args.dtype),
                    "points_per_step": D["step_points"], "samples_per_gpu": B,
                    "input_function_points": w["M"], "hidden": m["n_attn_hidden_dim"], "experts": m["n_expert"],
                    "heads": m["n_head"], "blocks": m["n_attn_layers"], "mlp_layers": m["n_mlp_num_layers"],

@@ -26,9 +26,9 @@ namespace gnot {
 
 // LDS of one workgroup (u32x4 units): two weight-chunk buffers, two 1 KiB bias buffers (layer parity,
 // forward) and per wave four 1 KiB slots of saved pre-activation tiles (backward).
-template <int D>
+template <int D, int NP>
 struct C2Lds {
-  static constexpr int WB = c2_tile_u4(D / 32);         // one output tile of a D x D x6 image
+  static constexpr int WB = c2_tile_u4(D / 32, NP);     // one output tile of a D x D image
   static constexpr int kBias = 2 * WB;                  // offset of the bias buffers
   static constexpr int kHs = kBias + 2 * 64;            // offset of the saved-row slots
   static constexpr int kBytes = (kHs + kC2Waves * 4 * 64) * 16;
@@ -50,12 +50,12 @@ struct C2Pipe {
 // + barrier, DMA of tile o+1 (or of the next layer's bias then tile 0), the 6 x KB MFMAs, then the
 // epilogue of tile o-1 (its save store is the ONLY vector-memory op after the DMA, so the next wait is
 // vmcnt(1)).
-template <int OT, int KBI, bool GELU, bool SAVE>
-GNOT_DEV void c2f_layer(C2Pipe& pp, const u32x4* W, const u32x4 (&in)[KBI][3], int bsel, rsrc_t rs, int voff,
+template <int OT, int KBI, bool GELU, bool SAVE, int NP>
+GNOT_DEV void c2f_layer(C2Pipe& pp, const u32x4* W, const u32x4 (&in)[KBI][NP], int bsel, rsrc_t rs, int voff,
                         const u32x4* nextW, int next_n16, const float* next_bias, int next_bias_bytes, int pend0,
                         int g, float (&out)[OT][4]) {
-  constexpr int TU = c2_tile_u4(KBI);
-  const u32x4* bias = pp.lds + C2Lds<256>::kBias + bsel * 64;
+  constexpr int TU = c2_tile_u4(KBI, NP);
+  const u32x4* bias = pp.lds + C2Lds<256, NP>::kBias + bsel * 64;
   f32x4 prev;
   auto epi = [&](int o, const f32x4& acc) {
     if (SAVE) buf_store_f32x4(make_float4(acc[0], acc[1], acc[2], acc[3]), rs, voff + 64 * o);
@@ -73,23 +73,23 @@ GNOT_DEV void c2f_layer(C2Pipe& pp, const u32x4* W, const u32x4 (&in)[KBI][3], i
     } else if (nextW) {
       // the next layer's bias first: the next layer's first wait only counts ops after its weights
       if (pp.wave == 0)
-        dma16(make_rsrc(next_bias, (unsigned)next_bias_bytes), pp.lds + C2Lds<256>::kBias + (bsel ^ 1) * 64,
+        dma16(make_rsrc(next_bias, (unsigned)next_bias_bytes), pp.lds + C2Lds<256, NP>::kBias + (bsel ^ 1) * 64,
               pp.lane * 16, 0);
       dma_image(pp.nxt(), nextW, next_n16, kC2Waves, pp.wave, pp.lane);
     }
     ++pp.cnt;
     const u32x4 bb = bias[4 * o + g];
-    const f32x4 acc = c2_tile<KBI, false>(cb, in, __builtin_bit_cast(f32x4, bb), pp.lane);
+    const f32x4 acc = c2_tile<KBI, false, NP>(cb, in, __builtin_bit_cast(f32x4, bb), pp.lane);
     if (o > 0) epi(o - 1, prev);
     prev = acc;
   }
   epi(OT - 1, prev);
 }
 
-template <int D, int KT0, int OTL, bool SAVE>
+template <int D, int KT0, int OTL, bool SAVE, int NP>
 __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) {
   constexpr int DT = D / 16, KB = DT / 2, KB0 = (KT0 + 1) / 2;
-  using LD = C2Lds<D>;
+  using LD = C2Lds<D, NP>;
   extern __shared__ __attribute__((aligned(16))) u32x4 c2lds[];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4;
   const long p = ((long)blockIdx.x * kC2Waves + wave) * 16 + (lane & 15);
@@ -102,33 +102,35 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) 
   C2Pipe pp{c2lds, LD::WB, 0, wave, lane};
   const u32x4* W0 = reinterpret_cast<const u32x4*>(L[0].Wp);
   if (wave == 0) dma16(make_rsrc(L[0].bias, 16 * DT * 4), c2lds + LD::kBias, lane * 16, 0);
-  dma_image(c2lds, W0, c2_tile_u4(KB0), kC2Waves, wave, lane);
+  dma_image(c2lds, W0, c2_tile_u4(KB0, NP), kC2Waves, wave, lane);
   auto wp = [&](int l) { return reinterpret_cast<const u32x4*>(L[l].Wp); };
   auto rs = [&](int l) { return make_rsrc(SAVE ? save + l * a.save_layer_stride : nullptr, SAVE ? lay_bytes : 0u); };
   constexpr int pend_next = SAVE ? 2 : 0;    // a layer's first wait: the previous layer's last two saves
 
   float nx[DT][4];                                   // next layer input (fp32), then split
-  u32x4 bp[KB][3];
+  u32x4 bp[KB][NP];
   int bsel = 0;
   {
     float x0[KT0][4];
     load_rows<KT0>(x0, a.X, a.ldx, p, valid, a.in_dim, lane);
-    u32x4 b0[KB0][3];
-    c2_split<KT0>(x0, b0);
+    u32x4 b0[KB0][NP];
+    c2_split<KT0, NP>(x0, b0);
     const int nb = nl - 1 == 1 ? 16 * OTL * 4 : 16 * DT * 4;
-    c2f_layer<DT, KB0, true, SAVE>(pp, W0, b0, bsel, rs(0), voff, wp(1), c2_tile_u4(KB), L[1].bias, nb, 0, g, nx);
+    c2f_layer<DT, KB0, true, SAVE, NP>(pp, W0, b0, bsel, rs(0), voff, wp(1), c2_tile_u4(KB, NP), L[1].bias, nb, 0, g,
+                                       nx);
     bsel ^= 1;
   }
   for (int l = 1; l < nl - 1; ++l) {
-    c2_split<DT>(nx, bp);
+    c2_split<DT, NP>(nx, bp);
     const int nb = l + 1 == nl - 1 ? 16 * OTL * 4 : 16 * DT * 4;
-    c2f_layer<DT, KB, true, SAVE>(pp, wp(l), bp, bsel, rs(l), voff, wp(l + 1), c2_tile_u4(KB), L[l + 1].bias, nb,
-                                  pend_next, g, nx);
+    c2f_layer<DT, KB, true, SAVE, NP>(pp, wp(l), bp, bsel, rs(l), voff, wp(l + 1), c2_tile_u4(KB, NP), L[l + 1].bias,
+                                      nb, pend_next, g, nx);
     bsel ^= 1;
   }
   float y[OTL][4];
-  c2_split<DT>(nx, bp);
-  c2f_layer<OTL, KB, false, SAVE>(pp, wp(nl - 1), bp, bsel, rs(nl - 1), voff, nullptr, 0, nullptr, 0, pend_next, g, y);
+  c2_split<DT, NP>(nx, bp);
+  c2f_layer<OTL, KB, false, SAVE, NP>(pp, wp(nl - 1), bp, bsel, rs(nl - 1), voff, nullptr, 0, nullptr, 0, pend_next, g,
+                                      y);
   if (a.mode == CH_SOFTMAX) {
     // softmax over the first out_dim outputs (features 16T + 4g + r); padded features excluded
     float m = -INFINITY;
@@ -171,11 +173,11 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) 
 // two tiles ahead into this wave's four slots (tile o in slot o % 4; the next layer's tiles 0 and 1
 // are requested by this layer's last two tiles).  Entry: the layer's tile-0 weights in pp.cur(), its
 // h tiles 0 and 1 requested, `pend0` vector-memory ops issued after its tile-0 weight DMA.
-template <int KBI>
-GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][3], rsrc_t rh, rsrc_t rz, rsrc_t rh_next,
+template <int KBI, int NP>
+GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP], rsrc_t rh, rsrc_t rz, rsrc_t rh_next,
                         bool has_next_h, int voff, const u32x4* nextW, int next_n16, int pend0, float (&nx)[16][4]) {
-  constexpr int DT = 16, TU = c2_tile_u4(KBI);
-  u32x4* slots = pp.lds + C2Lds<256>::kHs + pp.wave * 4 * 64;
+  constexpr int DT = 16, TU = c2_tile_u4(KBI, NP);
+  u32x4* slots = pp.lds + C2Lds<256, NP>::kHs + pp.wave * 4 * 64;
   f32x4 prev;
   auto epi = [&](int o, const f32x4& acc) {
     const float4 hc = lds_read16_sync(slots + (o & 3) * 64 + pp.lane);
@@ -200,7 +202,7 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][3], 
     ++pp.cnt;
     if (o + 2 < DT) dma16(rh, slots + ((o + 2) & 3) * 64, voff, 64 * (o + 2));
     else if (has_next_h) dma16(rh_next, slots + ((o + 2) & 3) * 64, voff, 64 * (o + 2 - DT));
-    const f32x4 acc = c2_tile<KBI, false>(cb, in, f32x4{0.f, 0.f, 0.f, 0.f}, pp.lane);
+    const f32x4 acc = c2_tile<KBI, false, NP>(cb, in, f32x4{0.f, 0.f, 0.f, 0.f}, pp.lane);
     if (o > 0) epi(o - 1, prev);
     prev = acc;
     __builtin_amdgcn_sched_barrier(0);      // no code motion across tiles (register pressure)
@@ -208,10 +210,10 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][3], 
   epi(DT - 1, prev);
 }
 
-template <int D, int KT0, int OTL>
+template <int D, int KT0, int OTL, int NP>
 __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) {
   constexpr int DT = D / 16, KB = DT / 2, KBL = (OTL + 1) / 2;
-  using LD = C2Lds<D>;
+  using LD = C2Lds<D, NP>;
   extern __shared__ __attribute__((aligned(16))) u32x4 c2lds[];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4;
   const long p = ((long)blockIdx.x * kC2Waves + wave) * 16 + (lane & 15);
@@ -227,7 +229,7 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) 
   auto rh = [&](int l) { return make_rsrc(save + l * a.save_layer_stride, lay_bytes); };   // h_l
   auto rz = [&](int l) { return make_rsrc(dz + l * a.dz_layer_stride, lay_bytes); };      // dz_l
   // prologue DMA: the last Linear's tile-0 weights and the first two h_{nl-2} tiles
-  dma_image(c2lds, wt(nl - 1), c2_tile_u4(KBL), kC2Waves, wave, lane);
+  dma_image(c2lds, wt(nl - 1), c2_tile_u4(KBL, NP), kC2Waves, wave, lane);
   {
     u32x4* slots = c2lds + LD::kHs + wave * 4 * 64;
     const rsrc_t r = rh(nl - 2);
@@ -276,24 +278,24 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) 
   store_rows<OTL>(dy, dz + (nl - 1) * a.dz_layer_stride, D, p, valid, 16 * OTL, lane);
 
   float nx[DT][4];
-  u32x4 bp[KB][3];
+  u32x4 bp[KB][NP];
   // next image after layer l's tiles: layer l-1's W^T, or the first Linear's (dX) when l - 1 == 0
   auto next_img = [&](int l) -> const u32x4* { return (l - 1 >= 1 || a.dX) ? wt(l - 1) : nullptr; };
   {
-    u32x4 bl[KBL][3];
-    c2_split<OTL>(dy, bl);
+    u32x4 bl[KBL][NP];
+    c2_split<OTL, NP>(dy, bl);
     const int l = nl - 1;
-    c2b_layer<KBL>(pp, wt(l), bl, rh(l - 1), rz(l - 1), rh(l >= 2 ? l - 2 : 0), l - 1 >= 1, voff, next_img(l),
-                   c2_tile_u4(KB), 0, nx);
+    c2b_layer<KBL, NP>(pp, wt(l), bl, rh(l - 1), rz(l - 1), rh(l >= 2 ? l - 2 : 0), l - 1 >= 1, voff, next_img(l),
+                       c2_tile_u4(KB, NP), 0, nx);
   }
   for (int l = nl - 2; l >= 1; --l) {
-    c2_split<DT>(nx, bp);
-    c2b_layer<KB>(pp, wt(l), bp, rh(l - 1), rz(l - 1), rh(l >= 2 ? l - 2 : 0), l - 1 >= 1, voff, next_img(l),
-                  c2_tile_u4(KB), 3, nx);
+    c2_split<DT, NP>(nx, bp);
+    c2b_layer<KB, NP>(pp, wt(l), bp, rh(l - 1), rz(l - 1), rh(l >= 2 ? l - 2 : 0), l - 1 >= 1, voff, next_img(l),
+                      c2_tile_u4(KB, NP), 3, nx);
   }
   // ---- first Linear: dX = W_0^T dz_0 (KT0 output tiles); first wait: the last layer's two dz stores
   if (a.dX) {
-    c2_split<DT>(nx, bp);
+    c2_split<DT, NP>(nx, bp);
     const u32x4* W0 = wt(0);
     float dx[KT0][4];
 #pragma unroll
@@ -301,9 +303,10 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) 
       if (o == 0) c2_sync<2>();
       else c2_sync<0>();
       const u32x4* cb = pp.cur();
-      if (o + 1 < KT0) dma_image(pp.nxt(), W0 + (size_t)(o + 1) * c2_tile_u4(KB), c2_tile_u4(KB), kC2Waves, wave, lane);
+      if (o + 1 < KT0)
+        dma_image(pp.nxt(), W0 + (size_t)(o + 1) * c2_tile_u4(KB, NP), c2_tile_u4(KB, NP), kC2Waves, wave, lane);
       ++pp.cnt;
-      f32x4 acc = c2_tile<KB, false>(cb, bp, f32x4{0.f, 0.f, 0.f, 0.f}, lane);
+      f32x4 acc = c2_tile<KB, false, NP>(cb, bp, f32x4{0.f, 0.f, 0.f, 0.f}, lane);
 #pragma unroll
       for (int r = 0; r < 4; ++r) dx[o][r] = acc[r];
     }
@@ -311,27 +314,27 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) 
   }
 }
 
-template <int D>
+template <int D, int NP>
 static hipError_t launch_chain2_d(const ChainArgs& a, bool bwd, hipStream_t s) {
   constexpr int DT = D / 16;
   const dim3 grid((a.P + 16 * kC2Waves - 1) / (16 * kC2Waves), a.nchains), block(64 * kC2Waves);
-  const size_t lds = C2Lds<D>::kBytes;
-#define GNOT_C2_CASE(K0, OL)                                                                         \
-  if (a.KT0 == K0 && a.OTL == OL) {                                                                  \
-    static bool attr = false;                                                                        \
-    if (!attr) {                                                                                     \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(chain2_bwd_kernel<D, K0, OL>),         \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);               \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(chain2_fwd_kernel<D, K0, OL, true>),   \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);               \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(chain2_fwd_kernel<D, K0, OL, false>),  \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);               \
-      attr = true;                                                                                   \
-    }                                                                                                \
-    if (bwd) hipLaunchKernelGGL((chain2_bwd_kernel<D, K0, OL>), grid, block, lds, s, a);             \
-    else if (a.save) hipLaunchKernelGGL((chain2_fwd_kernel<D, K0, OL, true>), grid, block, lds, s, a); \
-    else hipLaunchKernelGGL((chain2_fwd_kernel<D, K0, OL, false>), grid, block, lds, s, a);          \
-    return hipGetLastError();                                                                        \
+  const size_t lds = C2Lds<D, NP>::kBytes;
+#define GNOT_C2_CASE(K0, OL)                                                                             \
+  if (a.KT0 == K0 && a.OTL == OL) {                                                                      \
+    static bool attr = false;                                                                            \
+    if (!attr) {                                                                                         \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(chain2_bwd_kernel<D, K0, OL, NP>),         \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                   \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(chain2_fwd_kernel<D, K0, OL, true, NP>),   \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                   \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(chain2_fwd_kernel<D, K0, OL, false, NP>),  \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                   \
+      attr = true;                                                                                       \
+    }                                                                                                    \
+    if (bwd) hipLaunchKernelGGL((chain2_bwd_kernel<D, K0, OL, NP>), grid, block, lds, s, a);             \
+    else if (a.save) hipLaunchKernelGGL((chain2_fwd_kernel<D, K0, OL, true, NP>), grid, block, lds, s, a); \
+    else hipLaunchKernelGGL((chain2_fwd_kernel<D, K0, OL, false, NP>), grid, block, lds, s, a);          \
+    return hipGetLastError();                                                                            \
   }
   GNOT_C2_CASE(1, 1)
   GNOT_C2_CASE(1, DT)
@@ -345,7 +348,7 @@ hipError_t launch_chain2(const ChainArgs& a, bool bwd, hipStream_t s) {
   if (a.P <= 0 || a.nchains <= 0) return hipSuccess;
   if (a.nlin < 2) return hipErrorInvalidValue;
   switch (a.D) {
-    case 256: return launch_chain2_d<256>(a, bwd, s);
+    case 256: return a.np == 1 ? launch_chain2_d<256, 1>(a, bwd, s) : launch_chain2_d<256, 3>(a, bwd, s);
     default: return hipErrorInvalidValue;
   }
 }

@@ -179,6 +179,9 @@ struct gnot_plan {
   // input; the backward re-runs that call's expert forward into ONE shared save buffer ("mrsave")
   // just before its chain backward -- E*NL*P*D floats once instead of per MoE call
   bool moe_recompute = false;
+  // operand pieces of the d = 256 bf16-MFMA kernels (chain2, linear2, wide weight gradients):
+  // 3 = bf16x6 (fp32-exact, default), 1 = bf16 arithmetic mode (gnot_plan_set_precision)
+  int np = 3;
   std::string msave(int l, bool m1) const {
     return moe_recompute ? std::string("mrsave") : "b" + std::to_string(l) + (m1 ? ".m1save" : ".m2save");
   }
@@ -389,13 +392,13 @@ static void plan_images(gnot_plan* p) {
     p->packed4 += (size_t)OT * KT * 64;
     return im;
   };
-  // bf16x6 image (chain kernels): OT x ceil(KT/2) blocks of 3 pieces x 64 lanes x 16 B
-  auto new_img_x6 = [&](int OT, int KT) {
+  // bf16x6 image (chain kernels): OT x ceil(KT/2) blocks of `np` pieces x 64 lanes x 16 B
+  auto new_img_x6 = [&](int OT, int KT, int np = 3) {
     Img im;
     im.off4 = p->packed4;
     im.OT = OT;
     im.KT = KT;
-    p->packed4 += (size_t)OT * ((KT + 1) / 2) * 3 * 64;
+    p->packed4 += (size_t)OT * ((KT + 1) / 2) * np * 64;
     return im;
   };
   auto new_bias = [&](int n) {
@@ -421,16 +424,18 @@ static void plan_images(gnot_plan* p) {
   // d = 256: chain2.hip, bf16x6 output-major images in both directions; else chain.hip, k-major x6
   // forward image + exact fp32 backward-data image
   const bool c2 = p->D == 256;
+  const int c2np = c2 ? p->np : 3;                 // pieces of the output-major images
+  const int c2x6 = c2np == 1 ? 3 : 2;              // their pack mode
   auto chain_imgs = [&](int first, int KT0, int OTL) {
     for (int j = 0; j < NL; ++j) {
       const int li = first + j;
       const int KTp = (j == 0) ? KT0 : DT;
       const int OTp = (j == NL - 1) ? OTL : DT;
-      Img f = new_img_x6(OTp, KTp);
+      Img f = new_img_x6(OTp, KTp, c2np);
       const size_t bo = new_bias(16 * OTp);
-      job(li, f, 0, 0, OTp, KTp, 0, (long)bo, c2 ? 2 : 1);
-      Img t = c2 ? new_img_x6(KTp, OTp) : new_img(KTp, OTp);   // backward-data image
-      job(li, t, 0, 0, KTp, OTp, 1, -1, c2 ? 2 : 0);
+      job(li, f, 0, 0, OTp, KTp, 0, (long)bo, c2 ? c2x6 : 1);
+      Img t = c2 ? new_img_x6(KTp, OTp, c2np) : new_img(KTp, OTp);   // backward-data image
+      job(li, t, 0, 0, KTp, OTp, 1, -1, c2 ? c2x6 : 0);
       p->fwd_img[li] = f;
       p->T_img[li] = t;
       p->fwd_bias[li] = bo;
@@ -448,8 +453,8 @@ static void plan_images(gnot_plan* p) {
   auto attn_imgs = [&](gnot_plan::AttnImgs& A, int iq, int io, const std::vector<int>& ik,
                        const std::vector<int>& iv, bool selftype) {
     const int D = p->D;
-    const int x6 = c2 ? 2 : 0;
-    auto img = [&](int OT, int KT) { return c2 ? new_img_x6(OT, KT) : new_img(OT, KT); };
+    const int x6 = c2 ? c2x6 : 0;
+    auto img = [&](int OT, int KT) { return c2 ? new_img_x6(OT, KT, c2np) : new_img(OT, KT); };
     if (selftype) {
       A.qkv = img(3 * DT, DT);
       A.bqkv = new_bias(3 * D);
@@ -932,6 +937,18 @@ extern "C" int gnot_plan_set_shard(gnot_plan* p, int rank, int world, int B, con
   return GNOT_OK;
 }
 
+extern "C" int gnot_plan_set_precision(gnot_plan* p, int bf16) {
+  if (!p) return fail(GNOT_E_INVALID, "null plan");
+  const int np = bf16 ? 1 : 3;
+  if (p->np != np) {
+    p->np = np;
+    p->batch_set = false;          // image sizes change: set_batch + bind again
+    p->ws_bound = false;
+    p->packed = false;
+  }
+  return GNOT_OK;
+}
+
 extern "C" int gnot_plan_set_moe_recompute(gnot_plan* p, int on) {
   if (!p) return fail(GNOT_E_INVALID, "null plan");
   if (p->moe_recompute != (on != 0)) {
@@ -1355,7 +1372,7 @@ int run_linear(Ctx& c, const float* X, long ldx, int K, const Img& A, const floa
   LinearArgs a{};
   a.nseg = 1; a.X[0] = X; a.Wp[0] = A.p; a.ldx = ldx; a.nsum = 1; a.sum_stride = 0; a.K = K;
   a.bias = bias; a.Y = Y; a.ldy = ldy; a.NO = NO; a.P = (int)P;
-  a.epi = epi; a.nsoft = nsoft; a.dh = c.p->dh;
+  a.epi = epi; a.nsoft = nsoft; a.dh = c.p->dh; a.np = c.p->np;
   GNOT_CK(c.p->D == 256 ? launch_linear2(a, c.s) : launch_linear(a, c.p->D, c.s));
   return GNOT_OK;
 }
@@ -1371,7 +1388,7 @@ int run_linear_seg(Ctx& c, std::initializer_list<std::pair<const float*, const I
     ++a.nseg;
   }
   a.ldx = ldx; a.nsum = 1; a.K = c.p->D; a.bias = nullptr; a.Y = Y; a.ldy = ldy; a.NO = c.p->D; a.P = (int)P;
-  a.epi = epi; a.nsoft = 0; a.dh = c.p->dh;
+  a.epi = epi; a.nsoft = 0; a.dh = c.p->dh; a.np = c.p->np;
   GNOT_CK(c.p->D == 256 ? launch_linear2(a, c.s) : launch_linear(a, c.p->D, c.s));
   return GNOT_OK;
 }
@@ -1380,6 +1397,7 @@ ChainArgs chain_args(gnot_plan* p, const ChainTable& T, long P) {
   ChainArgs a{};
   a.D = p->D; a.KT0 = T.KT0; a.OTL = T.OTL; a.nlin = p->NL;
   a.in_dim = T.in_dim; a.out_dim = T.out_dim; a.P = (int)P; a.nchains = T.nchains; a.layers = T.dev;
+  a.np = p->np;
   return a;
 }
 
@@ -1436,7 +1454,7 @@ int run_wgrad_side(Ctx& c, const WgradGroup& G, std::initializer_list<const floa
     float* slab = c.s == p->side2 ? p->P_("slab_wgrad2") : p->P_("slab_wgrad");
     ProfScope ps(c, "wgrad", group_flops(G));
     GNOT_CK(launch_wgrad(G.d_jobs, G.d_wg_prefix, (int)G.jobs.size(), G.total_wgs, G.d_red_prefix,
-                         G.total_red, slab, c.s, G.x6, G.wide));
+                         G.total_red, slab, c.s, G.x6, G.wide, p->np));
     return GNOT_OK;
   }
   hipEvent_t fork = next_event(p);
@@ -1445,7 +1463,7 @@ int run_wgrad_side(Ctx& c, const WgradGroup& G, std::initializer_list<const floa
   {
     ProfScope ps(c, "wgrad", group_flops(G), p->side);
     GNOT_CK(launch_wgrad(G.d_jobs, G.d_wg_prefix, (int)G.jobs.size(), G.total_wgs, G.d_red_prefix,
-                         G.total_red, p->P_("slab_wgrad"), p->side, G.x6, G.wide));
+                         G.total_red, p->P_("slab_wgrad"), p->side, G.x6, G.wide, p->np));
   }
   hipEvent_t done = next_event(p);
   GNOT_CK(hipEventRecord(done, p->side));

@@ -351,16 +351,33 @@ GNOT_DEV void split8_x6(const float (&v)[8], u32x4 (&p)[3]) {
   }
 }
 
+// round-to-nearest-even bf16 of a float (bf16 arithmetic mode: one piece instead of three)
+GNOT_DEV unsigned bf16_rne_bits(float x) {
+  const unsigned u = f2u(x);
+  return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
+}
+// 8 floats -> 8 RNE bf16 (4 dwords, element j in the low half of dword j/2 for even j)
+GNOT_DEV void split8_bf16(const float (&v)[8], u32x4 (&p)[1]) {
+#pragma unroll
+  for (int d = 0; d < 4; ++d) p[0][d] = (bf16_rne_bits(v[2 * d + 1]) << 16) | bf16_rne_bits(v[2 * d]);
+}
+// NP = 3: the exact bf16x6 split; NP = 1: RNE bf16
+template <int NP>
+GNOT_DEV void split8_np(const float (&v)[8], u32x4 (&p)[NP]) {
+  if constexpr (NP == 3) split8_x6(v, p);
+  else split8_bf16(v, p);
+}
+
 // B pieces of k-block t of the point-form activations in[KT][4]: bp[q] = 8 bf16 (4 dwords) of piece q
-template <int KT>
-GNOT_DEV void split_block_x6(const float (&in)[KT][4], int t, u32x4 (&bp)[3]) {
+template <int KT, int NP = 3>
+GNOT_DEV void split_block_x6(const float (&in)[KT][4], int t, u32x4 (&bp)[NP]) {
   float v[8];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     v[j] = in[2 * t][j];
     v[4 + j] = (2 * t + 1 < KT) ? in[2 * t + 1][j] : 0.f;
   }
-  split8_x6(v, bp);
+  split8_np<NP>(v, bp);
 }
 
 GNOT_DEV f32x4 mfma_bf16(const u32x4& a, const u32x4& b, f32x4 c) {

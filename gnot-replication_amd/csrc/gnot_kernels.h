@@ -23,7 +23,7 @@ struct PackJob {
   int o0, t0, ktot;
   int OTp, KTp;        // tile counts of this job's image (>= what out/in need; the rest is zero)
   int x6;              // 1: bf16x6 image (3 bf16 pieces per 16x32 block, k-major, gnot_common.h); 2: the
-                       //    same output-major (chain2.hip); 0: fp32
+                       //    same output-major (chain2.hip); 3: output-major, 1 RNE bf16 piece; 0: fp32
   int otot;            // x6: output tiles of the whole image (its k-major block stride)
 };
 // pack tiles of a job: fp32 images have OTp*KTp tiles, x6 images OTp*ceil(KTp/2) blocks
@@ -50,6 +50,7 @@ struct LinearArgs {
   int epi;                           // LinearEpi
   int nsoft;                         // feature-softmax on output columns [0, nsoft)
   int dh;                            // head width for that softmax
+  int np = 3;                        // linear2: operand pieces (3 = bf16x6, 1 = bf16 mode)
 };
 hipError_t launch_linear(const LinearArgs& a, int D, hipStream_t s);
 // d = 256 projections on bf16x6 MFMA (linear2.hip): Wp[s] are OUTPUT-MAJOR x6 images (pack x6 = 2)
@@ -84,6 +85,7 @@ struct ChainArgs {
   float* dscore;                     // CH_MOE: dscore[p*ldsc + chain] += dq . y ; CH_SOFTMAX: d(scores)
   float* dz; long dz_layer_stride; long dz_chain_stride;          // per layer dZ [P, D] for wgrad
   float* dX; long lddx; long dx_chain_stride;                     // chain input grad or null
+  int np = 3;                        // d = 256: operand pieces (3 = bf16x6 fp32-exact, 1 = bf16 mode)
 };
 hipError_t launch_chain_fwd(const ChainArgs& a, hipStream_t s);
 hipError_t launch_chain_bwd(const ChainArgs& a, hipStream_t s);
@@ -116,7 +118,7 @@ struct WgradJob {
 //       wg_prefix counts splits only)
 hipError_t launch_wgrad(const WgradJob* jobs_dev, const int* wg_prefix_dev, int njobs, int total_wgs,
                         const int* red_prefix_dev, int total_red, float* slab, hipStream_t s, bool x6 = false,
-                        bool wide = false);
+                        bool wide = false, int np = 3);   // np: the wide kernel's operand pieces (1 = bf16 mode)
 
 // ------------------------------------------------------------------ attention states (state.hip)
 // Jobs are WgradJobs with state_dh > 0: A = dz/lddz, B = x/ldx, optional w/ldw, out = dW as

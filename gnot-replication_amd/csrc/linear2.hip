@@ -15,7 +15,7 @@
 
 namespace gnot {
 
-template <int TPH>   // output tiles per softmax head (dh / 16)
+template <int TPH, int NP>   // output tiles per softmax head (dh / 16); operand pieces (3 = x6, 1 = bf16)
 __global__ void __launch_bounds__(64 * kC2Waves) linear2_kernel(LinearArgs a) {
   constexpr int DT = 16, KB = 8;
   extern __shared__ __attribute__((aligned(16))) u32x4 c2lds[];
@@ -24,14 +24,14 @@ __global__ void __launch_bounds__(64 * kC2Waves) linear2_kernel(LinearArgs a) {
   const bool valid = p < a.P;
   const int OT = a.NO / 16;
   const u32x4* W = reinterpret_cast<const u32x4*>(a.Wp[0]);
-  C2Stream st{c2lds, c2_tile_u4(KB), 0, wave, lane};
-  stage_image(reinterpret_cast<float4*>(c2lds), reinterpret_cast<const float4*>(W), c2_tile_u4(KB), kC2Waves, wave,
-              lane);
-  u32x4 bp[KB][3];
+  C2Stream st{c2lds, c2_tile_u4(KB, NP), 0, wave, lane};
+  stage_image(reinterpret_cast<float4*>(c2lds), reinterpret_cast<const float4*>(W), c2_tile_u4(KB, NP), kC2Waves,
+              wave, lane);
+  u32x4 bp[KB][NP];
   {
     float x[DT][4];
     load_rows<DT>(x, a.X[0], a.ldx, p, valid, a.K, lane);
-    c2_split<DT>(x, bp);
+    c2_split<DT, NP>(x, bp);
   }
   // bias of the next head group and the old output rows (EPI_ACCUM) are loaded one group ahead / before
   // the MFMAs: a load placed after a barrier would expose its full latency on every tile
@@ -51,8 +51,8 @@ __global__ void __launch_bounds__(64 * kC2Waves) linear2_kernel(LinearArgs a) {
 #pragma unroll
     for (int k = 0; k < TPH; ++k) {
       const int o = o0 + k;
-      const u32x4* cb = st.begin(W, o, OT, c2_tile_u4(KB), nullptr, 0);
-      const f32x4 acc = c2_tile<KB>(cb, bp, f32x4{bc[k].x, bc[k].y, bc[k].z, bc[k].w}, lane);
+      const u32x4* cb = st.begin(W, o, OT, c2_tile_u4(KB, NP), nullptr, 0);
+      const f32x4 acc = c2_tile<KB, true, NP>(cb, bp, f32x4{bc[k].x, bc[k].y, bc[k].z, bc[k].w}, lane);
 #pragma unroll
       for (int r = 0; r < 4; ++r) h[k][r] = acc[r];
     }
@@ -87,15 +87,16 @@ __global__ void __launch_bounds__(64 * kC2Waves) linear2_kernel(LinearArgs a) {
   }
 }
 
+template <int NP>
 __global__ void __launch_bounds__(64 * kC2Waves) linear2_seg_kernel(LinearArgs a) {
   constexpr int DT = 16, KB = 8;
   extern __shared__ __attribute__((aligned(16))) u32x4 c2lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
   const long p = ((long)blockIdx.x * kC2Waves + wave) * 16 + (lane & 15);
   const bool valid = p < a.P;
-  C2Stream st{c2lds, c2_tile_u4(KB), 0, wave, lane};
-  stage_image(reinterpret_cast<float4*>(c2lds), reinterpret_cast<const float4*>(a.Wp[0]), c2_tile_u4(KB), kC2Waves,
-              wave, lane);
+  C2Stream st{c2lds, c2_tile_u4(KB, NP), 0, wave, lane};
+  stage_image(reinterpret_cast<float4*>(c2lds), reinterpret_cast<const float4*>(a.Wp[0]), c2_tile_u4(KB, NP),
+              kC2Waves, wave, lane);
   f32x4 acc[DT];
 #pragma unroll
   for (int o = 0; o < DT; ++o) {
@@ -107,18 +108,18 @@ __global__ void __launch_bounds__(64 * kC2Waves) linear2_seg_kernel(LinearArgs a
     }
   }
   for (int s = 0; s < a.nseg; ++s) {
-    u32x4 bp[KB][3];
+    u32x4 bp[KB][NP];
     {
       float x[DT][4];
       load_rows<DT>(x, a.X[s], a.ldx, p, valid, a.K, lane);
-      c2_split<DT>(x, bp);
+      c2_split<DT, NP>(x, bp);
     }
     const u32x4* W = reinterpret_cast<const u32x4*>(a.Wp[s]);
     const u32x4* next = s + 1 < a.nseg ? reinterpret_cast<const u32x4*>(a.Wp[s + 1]) : nullptr;
 #pragma unroll
     for (int o = 0; o < DT; ++o) {
-      const u32x4* cb = st.begin(W, o, DT, c2_tile_u4(KB), next, c2_tile_u4(KB));
-      acc[o] = c2_tile<KB, false>(cb, bp, acc[o], lane);
+      const u32x4* cb = st.begin(W, o, DT, c2_tile_u4(KB, NP), next, c2_tile_u4(KB, NP));
+      acc[o] = c2_tile<KB, false, NP>(cb, bp, acc[o], lane);
     }
   }
   if (valid) {
@@ -140,27 +141,32 @@ bool linear2_supported(const LinearArgs& a, int D) {
          (a.nseg == 1 ? (a.nsoft == 0 || a.dh == 16 || a.dh == 32 || a.dh == 64) : (a.NO == 256 && a.nsoft == 0));
 }
 
-hipError_t launch_linear2(const LinearArgs& a, hipStream_t s) {
-  if (a.P <= 0) return hipSuccess;
-  if (!linear2_supported(a, 256)) return hipErrorInvalidValue;
-  const size_t lds = 2 * (size_t)c2_tile_u4(8) * 16;
+template <int NP>
+static hipError_t launch_linear2_np(const LinearArgs& a, hipStream_t s) {
+  const size_t lds = 2 * (size_t)c2_tile_u4(8, NP) * 16;
   const dim3 grid((a.P + 16 * kC2Waves - 1) / (16 * kC2Waves)), block(64 * kC2Waves);
   static bool attr = false;
   if (!attr) {
-    for (const void* f : {reinterpret_cast<const void*>(linear2_kernel<1>), reinterpret_cast<const void*>(linear2_kernel<2>),
-                          reinterpret_cast<const void*>(linear2_kernel<4>), reinterpret_cast<const void*>(linear2_seg_kernel)})
+    for (const void* f : {reinterpret_cast<const void*>(linear2_kernel<1, NP>), reinterpret_cast<const void*>(linear2_kernel<2, NP>),
+                          reinterpret_cast<const void*>(linear2_kernel<4, NP>), reinterpret_cast<const void*>(linear2_seg_kernel<NP>)})
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   if (a.nseg > 1) {
-    hipLaunchKernelGGL(linear2_seg_kernel, grid, block, lds, s, a);
+    hipLaunchKernelGGL(linear2_seg_kernel<NP>, grid, block, lds, s, a);
   } else {
     const int tph = a.nsoft ? a.dh / 16 : 2;
-    if (tph == 1) hipLaunchKernelGGL(linear2_kernel<1>, grid, block, lds, s, a);
-    else if (tph == 2) hipLaunchKernelGGL(linear2_kernel<2>, grid, block, lds, s, a);
-    else hipLaunchKernelGGL(linear2_kernel<4>, grid, block, lds, s, a);
+    if (tph == 1) hipLaunchKernelGGL((linear2_kernel<1, NP>), grid, block, lds, s, a);
+    else if (tph == 2) hipLaunchKernelGGL((linear2_kernel<2, NP>), grid, block, lds, s, a);
+    else hipLaunchKernelGGL((linear2_kernel<4, NP>), grid, block, lds, s, a);
   }
   return hipGetLastError();
+}
+
+hipError_t launch_linear2(const LinearArgs& a, hipStream_t s) {
+  if (a.P <= 0) return hipSuccess;
+  if (!linear2_supported(a, 256)) return hipErrorInvalidValue;
+  return a.np == 1 ? launch_linear2_np<1>(a, s) : launch_linear2_np<3>(a, s);
 }
 
 }  // namespace gnot

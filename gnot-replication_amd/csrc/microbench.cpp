@@ -86,6 +86,14 @@ int main(int argc, char** argv) {
   bw.dz_chain_stride = (long)NL * P * D; bw.dX = dX; bw.lddx = D; bw.dx_chain_stride = (long)P * D;
   t = time_us([&] { CK(launch_chain_bwd(bw, nullptr)); });
   std::printf("chain_bwd  MoE E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
+  if (D == 256) {   // bf16 arithmetic mode (one operand piece)
+    ChainArgs a1 = a, b1 = bw;
+    a1.np = 1; b1.np = 1;
+    t = time_us([&] { CK(launch_chain_fwd(a1, nullptr)); });
+    std::printf("chain_fwd  bf16 E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
+    t = time_us([&] { CK(launch_chain_bwd(b1, nullptr)); });
+    std::printf("chain_bwd  bf16 E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
+  }
 
   for (int NO : {D, 3 * D}) {
     LinearArgs l{};
@@ -93,6 +101,12 @@ int main(int argc, char** argv) {
     l.NO = NO; l.P = P; l.epi = EPI_STORE; l.nsoft = 0; l.dh = 16;
     t = time_us([&] { CK(D == 256 ? launch_linear2(l, nullptr) : launch_linear(l, D, nullptr)); });
     std::printf("linear     P=%d K=%d NO=%d: %8.2f us  %6.1f TFLOP/s\n", P, D, NO, t, 2.0 * P * D * NO / t / 1e6);
+    if (D == 256) {
+      l.np = 1;
+      t = time_us([&] { CK(launch_linear2(l, nullptr)); });
+      std::printf("linear     P=%d K=%d NO=%d bf16: %8.2f us  %6.1f TFLOP/s\n", P, D, NO, t, 2.0 * P * D * NO / t / 1e6);
+      l.np = 3;
+    }
     if (D == 256 && NO == D) {
       l.epi = EPI_ACCUM;
       t = time_us([&] { CK(launch_linear2(l, nullptr)); });
@@ -182,6 +196,13 @@ int main(int argc, char** argv) {
         double n2 = 0, d2 = 0;
         for (size_t i = 0; i < ndw; ++i) { n2 += (got[i] - ref[i]) * (double)(got[i] - ref[i]); d2 += (double)ref[i] * ref[i]; }
         std::printf("wgrad MoE  bf16x6 wide 256x256 (%d WGs):  %8.2f us  %6.1f TFLOP/s  (rel-L2 vs fp32 %.2e)\n",
+                    njobs * splits, t, fl / t / 1e6, std::sqrt(n2 / (d2 + 1e-30)));
+        t = time_us([&] { CK(launch_wgrad(dwj, dwpre, njobs, njobs * splits, dwpre + njobs, red, wslab, nullptr, true, true, 1)); }, 20);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(got.data(), dW, ndw * 4, hipMemcpyDeviceToHost));
+        n2 = 0; d2 = 0;
+        for (size_t i = 0; i < ndw; ++i) { n2 += (got[i] - ref[i]) * (double)(got[i] - ref[i]); d2 += (double)ref[i] * ref[i]; }
+        std::printf("wgrad MoE  bf16 wide 256x256 (%d WGs):    %8.2f us  %6.1f TFLOP/s  (rel-L2 vs fp32 %.2e)\n",
                     njobs * splits, t, fl / t / 1e6, std::sqrt(n2 / (d2 + 1e-30)));
         CK(hipFree(dwj));
         CK(hipFree(dwpre));

@@ -367,8 +367,10 @@ __global__ void __launch_bounds__(256) pgemm_x6_kernel(const WgradJob* __restric
 constexpr int kWStage = 16;
 constexpr int kWThreads = 512;
 constexpr int kWPiece = 8 * 64;                  // u32x4 per (operand, piece) image
-constexpr int kWBuf = 6 * kWPiece;               // A pieces 0..2 | B pieces 0..2
-constexpr size_t kWLdsBytes = 2 * kWBuf * 16;    // 96 KiB
+// one stage buffer: A pieces 0..NP-1 | B pieces 0..NP-1 (NP = 3: bf16x6, 1: bf16 mode)
+constexpr int w_buf(int np) { return 2 * np * kWPiece; }
+constexpr size_t w_lds_bytes(int np) { return 2 * (size_t)w_buf(np) * 16; }   // 96 KiB at NP = 3
+constexpr size_t kWLdsBytes = w_lds_bytes(3);
 
 GNOT_DEV void x6_mfma6(const u32x4 (&a)[3], const u32x4 (&b)[3], f32x16& c) {
 #define GNOT_MFMA32(X, Y) \
@@ -381,8 +383,13 @@ GNOT_DEV void x6_mfma6(const u32x4 (&a)[3], const u32x4 (&b)[3], f32x16& c) {
   GNOT_MFMA32(a[0], b[0]);
 #undef GNOT_MFMA32
 }
+template <int NP>
+GNOT_DEV void mfma_np(const u32x4 (&a)[NP], const u32x4 (&b)[NP], f32x16& c) {
+  if constexpr (NP == 3) x6_mfma6(a, b, c);
+  else c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[0]), __builtin_bit_cast(bf16x8, b[0]), c, 0, 0, 0);
+}
 
-template <int V>
+template <int V, int NP = 3>
 __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __restrict__ jobs,
                                                               const int* __restrict__ prefix, int njobs,
                                                               float* __restrict__ slab) {
@@ -442,14 +449,14 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
       dbacc += ra[k];
       vb[k] = decltype(GEL)::value ? gelu(b) : b;
     }
-    u32x4 pa[3], pq[3];
-    split8_x6(ra, pa);
-    split8_x6(vb, pq);
-    u32x4* base = wl + buf * kWBuf;
+    u32x4 pa[NP], pq[NP];
+    split8_np<NP>(ra, pa);
+    split8_np<NP>(vb, pq);
+    u32x4* base = wl + buf * w_buf(NP);
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
+    for (int q = 0; q < NP; ++q) {
       base[q * kWPiece + sdst] = pa[q];
-      base[(3 + q) * kWPiece + sdst] = pq[q];
+      base[(NP + q) * kWPiece + sdst] = pq[q];
     }
   };
   auto stage = [&](int buf, const Raw& R) {
@@ -457,37 +464,37 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
     else stage_v(buf, R, std::false_type{});
   };
   auto compute = [&](int buf) {
-    const u32x4* A = wl + buf * kWBuf;
-    const u32x4* Bm = A + 3 * kWPiece;
-    u32x4 bf[2][3];
+    const u32x4* A = wl + buf * w_buf(NP);
+    const u32x4* Bm = A + NP * kWPiece;
+    u32x4 bf[2][NP];
 #pragma unroll
     for (int jb = 0; jb < 2; ++jb)
 #pragma unroll
-      for (int q = 0; q < 3; ++q) bf[jb][q] = Bm[q * kWPiece + (wc * 2 + jb) * 64 + lane];
+      for (int q = 0; q < NP; ++q) bf[jb][q] = Bm[q * kWPiece + (wc * 2 + jb) * 64 + lane];
     if (full) {
       // row-block fragments one block ahead (two sets live: the register budget of two waves per SIMD)
-      u32x4 af[2][3];
+      u32x4 af[2][NP];
 #pragma unroll
-      for (int q = 0; q < 3; ++q) af[0][q] = A[q * kWPiece + (wr * 4) * 64 + lane];
+      for (int q = 0; q < NP; ++q) af[0][q] = A[q * kWPiece + (wr * 4) * 64 + lane];
 #pragma unroll
       for (int ib = 0; ib < 4; ++ib) {
         if (ib + 1 < 4) {
 #pragma unroll
-          for (int q = 0; q < 3; ++q) af[(ib + 1) & 1][q] = A[q * kWPiece + (wr * 4 + ib + 1) * 64 + lane];
+          for (int q = 0; q < NP; ++q) af[(ib + 1) & 1][q] = A[q * kWPiece + (wr * 4 + ib + 1) * 64 + lane];
         }
-        x6_mfma6(af[ib & 1], bf[0], acc[ib][0]);
-        x6_mfma6(af[ib & 1], bf[1], acc[ib][1]);
+        mfma_np<NP>(af[ib & 1], bf[0], acc[ib][0]);
+        mfma_np<NP>(af[ib & 1], bf[1], acc[ib][1]);
         __builtin_amdgcn_sched_barrier(0);
       }
     } else {
 #pragma unroll
       for (int ib = 0; ib < 4; ++ib) {
         if (ib >= nrb) break;
-        u32x4 af[3];
+        u32x4 af[NP];
 #pragma unroll
-        for (int q = 0; q < 3; ++q) af[q] = A[q * kWPiece + (wr * 4 + ib) * 64 + lane];
-        if (ncb > 0) x6_mfma6(af, bf[0], acc[ib][0]);
-        if (ncb > 1) x6_mfma6(af, bf[1], acc[ib][1]);
+        for (int q = 0; q < NP; ++q) af[q] = A[q * kWPiece + (wr * 4 + ib) * 64 + lane];
+        if (ncb > 0) mfma_np<NP>(af, bf[0], acc[ib][0]);
+        if (ncb > 1) mfma_np<NP>(af, bf[1], acc[ib][1]);
       }
     }
   };
@@ -611,9 +618,19 @@ __global__ void __launch_bounds__(256) pgemm_reduce_kernel(const WgradJob* __res
 }
 
 hipError_t launch_wgrad(const WgradJob* jobs_dev, const int* wg_prefix_dev, int njobs, int total_wgs,
-                        const int* red_prefix_dev, int total_red, float* slab, hipStream_t s, bool x6, bool wide) {
+                        const int* red_prefix_dev, int total_red, float* slab, hipStream_t s, bool x6, bool wide,
+                        int np) {
   if (njobs <= 0) return hipSuccess;
-  if (wide) {
+  if (wide && np == 1) {
+    static bool attr1 = false;
+    if (!attr1) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(pgemm_x6w_kernel<0, 1>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)w_lds_bytes(1));
+      attr1 = true;
+    }
+    hipLaunchKernelGGL((pgemm_x6w_kernel<0, 1>), dim3(total_wgs), dim3(kWThreads), w_lds_bytes(1), s, jobs_dev,
+                       wg_prefix_dev, njobs, slab);
+  } else if (wide) {
     // GNOT_X6W_VARIANT (diagnostics): bit 0 priority split, bit 1 two raw register sets
     static const int var = std::getenv("GNOT_X6W_VARIANT") ? std::atoi(std::getenv("GNOT_X6W_VARIANT")) & 3 : 0;
     static bool attr = false;

@@ -10,32 +10,37 @@ namespace gnot {
 
 constexpr int kC2Waves = 8;
 
-// u32x4 per output tile of an x6 image with KB k-blocks
-constexpr int c2_tile_u4(int KB) { return KB * 3 * WAVE; }
+// Piece count NP: 3 = the exact bf16x6 form (fp32 arithmetic), 1 = plain bf16 (RNE operands, fp32
+// accumulation: the bf16 arithmetic mode, gnot_plan_set_precision).
+// u32x4 per output tile of an image with KB k-blocks
+constexpr int c2_tile_u4(int KB, int NP = 3) { return KB * NP * WAVE; }
 
 // acc += sum_t W[o][t] . in[t] for one output tile: the weight pieces of k-block t+1 are read from
-// LDS while the six MFMAs of block t run (smallest terms first, one accumulator)
-template <int KB, bool AHEAD = true>
-GNOT_DEV f32x4 c2_tile(const u32x4* __restrict__ cb, const u32x4 (&bp)[KB][3], f32x4 acc, int lane) {
-  u32x4 a[AHEAD ? 2 : 1][3];
+// LDS while the MFMAs of block t run (x6: the six order <= 2 products, smallest terms first, one
+// accumulator; bf16: one product)
+template <int KB, bool AHEAD = true, int NP = 3>
+GNOT_DEV f32x4 c2_tile(const u32x4* __restrict__ cb, const u32x4 (&bp)[KB][NP], f32x4 acc, int lane) {
+  u32x4 a[AHEAD ? 2 : 1][NP];
 #pragma unroll
-  for (int q = 0; q < 3; ++q) a[0][q] = cb[q * WAVE + lane];
+  for (int q = 0; q < NP; ++q) a[0][q] = cb[q * WAVE + lane];
 #pragma unroll
   for (int t = 0; t < KB; ++t) {
     if (!AHEAD && t > 0) {
 #pragma unroll
-      for (int q = 0; q < 3; ++q) a[0][q] = cb[(t * 3 + q) * WAVE + lane];
+      for (int q = 0; q < NP; ++q) a[0][q] = cb[(t * NP + q) * WAVE + lane];
     }
     if (AHEAD && t + 1 < KB) {
 #pragma unroll
-      for (int q = 0; q < 3; ++q) a[(t + 1) & 1][q] = cb[((t + 1) * 3 + q) * WAVE + lane];
+      for (int q = 0; q < NP; ++q) a[(t + 1) & 1][q] = cb[((t + 1) * NP + q) * WAVE + lane];
     }
-    const u32x4(&w)[3] = a[AHEAD ? (t & 1) : 0];
-    acc = mfma_bf16(w[2], bp[t][0], acc);
-    acc = mfma_bf16(w[1], bp[t][1], acc);
-    acc = mfma_bf16(w[0], bp[t][2], acc);
-    acc = mfma_bf16(w[1], bp[t][0], acc);
-    acc = mfma_bf16(w[0], bp[t][1], acc);
+    const u32x4(&w)[NP] = a[AHEAD ? (t & 1) : 0];
+    if constexpr (NP == 3) {
+      acc = mfma_bf16(w[2], bp[t][0], acc);
+      acc = mfma_bf16(w[1], bp[t][1], acc);
+      acc = mfma_bf16(w[0], bp[t][2], acc);
+      acc = mfma_bf16(w[1], bp[t][0], acc);
+      acc = mfma_bf16(w[0], bp[t][1], acc);
+    }
     acc = mfma_bf16(w[0], bp[t][0], acc);
   }
   return acc;
@@ -112,10 +117,10 @@ GNOT_DEV void dma_image(u32x4* lds, const void* src, int n16, int nwaves, int wa
   for (int base = w * WAVE; base < n16; base += nwaves * WAVE) dma16(r, lds + base, lane * 16, base * 16);
 }
 
-template <int KT>
-GNOT_DEV void c2_split(const float (&v)[KT][4], u32x4 (&bp)[(KT + 1) / 2][3]) {
+template <int KT, int NP = 3>
+GNOT_DEV void c2_split(const float (&v)[KT][4], u32x4 (&bp)[(KT + 1) / 2][NP]) {
 #pragma unroll
-  for (int t = 0; t < (KT + 1) / 2; ++t) split_block_x6<KT>(v, t, bp[t]);
+  for (int t = 0; t < (KT + 1) / 2; ++t) split_block_x6<KT, NP>(v, t, bp[t]);
 }
 
 GNOT_DEV float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }

@@ -42,6 +42,7 @@ class Engine:
         self.param_grads = True    # False: no .grad tensors; grad_flat IS the arena (FlatAdamW reads it)
         self.comm = None           # parallel.PointShardComm when points are sharded over ranks
         self.moe_recompute = False # re-run each MoE call's expert forward in the backward (memory option)
+        self.bf16 = False          # bf16 arithmetic mode of the d = 256 MFMA kernels (gnot_plan_set_precision)
         self.fwd_token = 0
 
     def __del__(self):
@@ -70,7 +71,7 @@ class Engine:
         n_global: per-sample global point counts when the points are sharded over ranks (self.comm)."""
         self._bind_params()
         geom = (tuple(x_off), tuple(tuple(o) for o in fn_offs), bool(training),
-                tuple(n_global) if n_global is not None else None, bool(self.moe_recompute))
+                tuple(n_global) if n_global is not None else None, bool(self.moe_recompute), bool(self.bf16))
         if geom == self.geom:
             return
         B = len(x_off) - 1
@@ -86,6 +87,7 @@ class Engine:
         else:
             _lib.check(self.lib.gnot_plan_set_shard(self.plan, 0, 1, 0, None, None))
         _lib.check(self.lib.gnot_plan_set_moe_recompute(self.plan, int(bool(self.moe_recompute))))
+        _lib.check(self.lib.gnot_plan_set_precision(self.plan, int(bool(self.bf16))))
         xo = (ctypes.c_int64 * (B + 1))(*x_off)
         flat = [v for o in fn_offs for v in o]
         fo = (ctypes.c_int64 * max(1, len(flat)))(*flat) if flat else None

@@ -137,6 +137,7 @@ class GNOT(nn.Module):
         self._engine = None
         self._comm = None          # parallel.PointShardComm (set_point_shard); survives engine rebuilds
         self._moe_recompute = False
+        self._bf16 = False
 
     # canonical Linear order == named_parameters() order of the reference module
     def linears(self):
@@ -152,7 +153,22 @@ class GNOT(nn.Module):
             self._engine = Engine(self._cfg, self.linears())
             self._engine.comm = self._comm
             self._engine.moe_recompute = self._moe_recompute
+            self._engine.bf16 = self._bf16
         return self._engine
+
+    def set_precision(self, dtype):
+        """'fp32' (default: the reference's fp32 arithmetic, bf16x6-exact on the MFMA) or 'bf16' (BASELINE
+        configs[2]'s bf16 training: ONE round-to-nearest bf16 operand piece per MFMA in the d = 256 MLP
+        chains, attention projections and weight gradients, fp32 accumulation; parameters, activations
+        and the attention contractions stay fp32).  Other hidden widths are unaffected."""
+        d = str(dtype).replace("torch.", "")
+        if d in ("bf16", "bfloat16"):
+            self._bf16 = True
+        elif d in ("fp32", "float32", "float"):
+            self._bf16 = False
+        else:
+            raise ValueError(f"precision must be 'fp32' or 'bf16', got {dtype!r}")
+        self.engine().bf16 = self._bf16
 
     def set_moe_recompute(self, on=True):
         """Memory option (no reference counterpart; torch.utils.checkpoint is the analogue): keep only

@@ -83,6 +83,14 @@ int gnot_plan_set_batch(gnot_plan* plan, int B, const int64_t* x_off, const int6
  * memory option of this library; torch.utils.checkpoint is the analogue). */
 int gnot_plan_set_moe_recompute(gnot_plan* plan, int on);
 
+/* Arithmetic mode of the d = 256 MFMA kernels (MLP chains, attention projections, weight gradients):
+ * bf16 == 0 (default) runs them as bf16x6 -- three exact bf16 pieces per fp32 operand, six products,
+ * fp32-level results (north_star's 1e-4 bar); bf16 != 0 runs ONE round-to-nearest-even bf16 piece per
+ * operand with fp32 accumulation (BASELINE configs[2]'s bf16 training; north_star's 1e-2 bar).
+ * Activations, states, gradients and the attention contractions stay fp32 either way; other widths
+ * are unaffected.  Changing it invalidates the batch (set_batch + bind again). */
+int gnot_plan_set_precision(gnot_plan* plan, int bf16);
+
 /* Workspace: bytes needed for the current config + batch; bind a device buffer of at least that
  * size (256-byte aligned).  Binding uploads the plan's small device tables: gnot_plan_bind_workspace
  * synchronously; gnot_plan_bind_workspace_async as one copy from pinned staging ordered on `stream`
