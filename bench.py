@@ -41,6 +41,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_16x16x4_f32 / 32x32x2, dense
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: "Peak BF16/FP16 MFMA ~2.5 PF dense" (no sparsity)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -242,6 +243,8 @@ def main():
                     help="fp32: the reference's arithmetic (bf16x6-exact MFMA); bf16: configs[2]'s bf16 training "
                          "(one RNE bf16 operand per MFMA in the d=256 chains / projections / weight gradients, "
                          "fp32 accumulation and storage; north_star's 1e-2 bar, tests/test_gpu_bf16.py)")
+    ap.add_argument("--fp32-only", action="store_true",
+                    help="skip the companion bf16-mode measurement of the default fp32 run (configs[2], N=1)")
     ap.add_argument("--recompute", choices=["auto", "on", "off"], default="auto",
                     help="MoE activation recompute (GNOT.set_moe_recompute); auto: on when the plain workspace "
                          "would not fit the GPU (configs[3]'s 1M-point mesh on one GPU)")
@@ -361,83 +364,117 @@ def main():
             opt.prepare()
         opt_step()
 
-    # warm-up (also the capture warm-up: allocations, plan binding, optimizer state)
-    side = torch.cuda.Stream(device)
-    side.wait_stream(torch.cuda.current_stream(device))
-    with torch.cuda.stream(side):
-        for _ in range(max(args.warmup, 2)):
+    def roofline(M, dtype):
+        """the device-time-dominant kernel class of a measure() run against the dense MFMA peak of the
+        arithmetic it runs (fp32: the fp32 MFMA rate -- bf16x6 computes fp32; bf16: the bf16 rate)"""
+        avg_ms = M["kms"] / max(M["klaunch"], 1)
+        ach = (M["kflops"] / max(M["klaunch"], 1)) / (avg_ms * 1e-3) / 1e12 if M["klaunch"] and M["kms"] > 0 else 0.0
+        peak = FP32_MFMA_PEAK_TFLOPS if dtype == "fp32" else BF16_MFMA_PEAK_TFLOPS
+        form = "bf16x6" if dtype == "fp32" else "bf16"
+        names = ({"moe_fwd": f"chain2_fwd_kernel (fused MoE expert chains, forward, {form} MFMA)",
+                  "moe_bwd": f"chain2_bwd_kernel (fused MoE expert chains, backward, {form} MFMA)",
+                  "wgrad": f"pgemm_x6w_kernel+pgemm_reduce_kernel (weight gradients, 256x256 {form} MFMA)"}
+                 if m["n_attn_hidden_dim"] == 256 else
+                 {"moe_fwd": "chain_fwd_kernel (fused MoE expert chains, forward)",
+                  "moe_bwd": "chain_bwd_kernel (fused MoE expert chains, backward)",
+                  "wgrad": "pgemm_x6_kernel+pgemm_reduce_kernel (weight gradients, bf16x6 MFMA)"})
+        rk = M["rkind"]
+        return {
+            "kernel": names[rk],
+            "class": rk,
+            "class_ms_per_step": {k: round(v[0], 3) for k, v in M["kinds"].items()},
+            "bound": "mfma",
+            "achieved": round(ach, 3),
+            "peak": peak,
+            "unit": "TFLOP/s",
+            "frac": round(ach / peak, 4),
+            "traffic": None if (args.points or dtype != "fp32") else pmc_traffic(args.workload, rk),
+            "avg_launch_us": round(avg_ms * 1e3, 2),
+            "flops_per_launch": M["kflops"] / max(M["klaunch"], 1),
+            "launches": M["klaunch"],
+        }
+
+    def measure():
+        """warm-up, class profile, capture, K timed steps -> timing of the current precision"""
+        # warm-up (also the capture warm-up: allocations, plan binding, optimizer state)
+        side = torch.cuda.Stream(device)
+        side.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(side):
+            for _ in range(max(args.warmup, 2)):
+                eager_step()
+        torch.cuda.current_stream(device).wait_stream(side)
+        torch.cuda.synchronize()
+        print("[bench] warm-up done", file=sys.stderr, flush=True)
+        # which kernel class dominates device time: one profiled eager step per class (untimed)
+        kinds = {}
+        for kind in ("moe_fwd", "moe_bwd", "wgrad"):
+            eng.profile_enable(kind)
             eager_step()
-    torch.cuda.current_stream(device).wait_stream(side)
-    torch.cuda.synchronize()
-    print("[bench] warm-up done", file=sys.stderr, flush=True)
-    # which kernel class dominates device time: one profiled eager step per class (untimed)
-    kinds = {}
-    for kind in ("moe_fwd", "moe_bwd", "wgrad"):
-        eng.profile_enable(kind)
-        eager_step()
-        kinds[kind] = eng.profile_read()
-        if args.breakdown:
-            ms, n, fl = kinds[kind]
-            print(f"[breakdown] {kind}: {ms:.3f} ms/step over {n} launches, "
-                  f"{fl / ms / 1e9 if ms else 0:.1f} TFLOP/s", file=sys.stderr)
-    eng.profile_enable("")
-    torch.cuda.synchronize()
-    rkind = args.roofline_kernel
-    if rkind == "auto":
-        rkind = max(kinds, key=lambda k: kinds[k][0])
-
-    step = eager_step
-    if use_graph:
-        # the roofline kernel's hipEvent pairs are recorded inside the captured graph, so the timed
-        # replays carry them (the pool of events exists from one eager profiled step)
-        eng.profile_enable(rkind)
-        eager_step()
-        eng.profile_read()
+            kinds[kind] = eng.profile_read()
+            if args.breakdown:
+                ms, n, fl = kinds[kind]
+                print(f"[breakdown] {kind}: {ms:.3f} ms/step over {n} launches, "
+                      f"{fl / ms / 1e9 if ms else 0:.1f} TFLOP/s", file=sys.stderr)
+        eng.profile_enable("")
         torch.cuda.synchronize()
-        eng.profile_enable(rkind)
-        g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        print("[bench] capturing", file=sys.stderr, flush=True)
-        with torch.cuda.graph(g_fb):
-            fwd_bwd()
-        with torch.cuda.graph(g_opt, pool=g_fb.pool()):
-            opt_step()
-        torch.cuda.synchronize()
-        print("[bench] captured", file=sys.stderr, flush=True)
+        rkind = args.roofline_kernel
+        if rkind == "auto":
+            rkind = max(kinds, key=lambda k: kinds[k][0])
 
-        def graph_step():
-            g_fb.replay()
-            allreduce()
-            if not args.torch_adamw:
-                opt.prepare()         # this step's AdamW hyper-parameters -> device (outside the graph)
-            g_opt.replay()
-        step = graph_step
-        for _ in range(2):
+        step = eager_step
+        if use_graph:
+            # the roofline kernel's hipEvent pairs are recorded inside the captured graph, so the timed
+            # replays carry them (the pool of events exists from one eager profiled step)
+            eng.profile_enable(rkind)
+            eager_step()
+            eng.profile_read()
+            torch.cuda.synchronize()
+            eng.profile_enable(rkind)
+            g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            print("[bench] capturing", file=sys.stderr, flush=True)
+            with torch.cuda.graph(g_fb):
+                fwd_bwd()
+            with torch.cuda.graph(g_opt, pool=g_fb.pool()):
+                opt_step()
+            torch.cuda.synchronize()
+            print("[bench] captured", file=sys.stderr, flush=True)
+
+            def graph_step():
+                g_fb.replay()
+                allreduce()
+                if not args.torch_adamw:
+                    opt.prepare()         # this step's AdamW hyper-parameters -> device (outside the graph)
+                g_opt.replay()
+            step = graph_step
+            for _ in range(2):
+                step()
+            torch.cuda.synchronize()
+        else:
+            eng.profile_enable(rkind)
+
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
             step()
         torch.cuda.synchronize()
-    else:
-        eng.profile_enable(rkind)
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        # eager: summed over every timed step; graph: the events hold the LAST replay's launches, and
+        # launches/flops are those of one step -> both give the average launch duration
+        kms, klaunch, kflops = eng.profile_read()
+        eng.profile_enable("")
+        if world > 1:
+            t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        return dict(elapsed=elapsed, kinds=kinds, rkind=rkind, kms=kms, klaunch=klaunch, kflops=kflops)
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    # eager: summed over every timed step; graph: the events hold the LAST replay's launches, and
-    # launches/flops are those of one step -> both give the average launch duration
-    kms, klaunch, kflops = eng.profile_read()
-    eng.profile_enable("")
-    if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    M0 = measure()
+    elapsed, kinds, rkind, kms, klaunch, kflops = (M0[k] for k in ("elapsed", "kinds", "rkind", "kms", "klaunch", "kflops"))
     pts = D["step_points"] * args.steps
-    avg_launch_ms = kms / max(klaunch, 1)
-    achieved = (kflops / max(klaunch, 1)) / (avg_launch_ms * 1e-3) / 1e12 if klaunch and kms > 0 else 0.0
     result = {
         "metric": "mesh points/sec (GNOT fwd+bwd, whole node)",
         "value": round(pts / elapsed, 1),
@@ -461,27 +498,24 @@ def main():
                    "moe_recompute": recompute,
                    "parallelism": (f"point-shard{world}" if shard else f"sample-dp{world}") if world > 1 else "single",
                    "step": "pack+fwd+RelL2+bwd+AdamW (native loss, " + ("torch fused AdamW" if args.torch_adamw else "native flat AdamW") + ")" + (" (hipGraph replay)" if use_graph else " (eager)")},
-        "roofline": {
-            "kernel": ({"moe_fwd": "chain2_fwd_kernel (fused MoE expert chains, forward, bf16x6 MFMA)",
-                        "moe_bwd": "chain2_bwd_kernel (fused MoE expert chains, backward, bf16x6 MFMA)",
-                        "wgrad": "pgemm_x6w_kernel+pgemm_reduce_kernel (weight gradients, 256x256 bf16x6 MFMA)"}
-                       if m["n_attn_hidden_dim"] == 256 else
-                       {"moe_fwd": "chain_fwd_kernel (fused MoE expert chains, forward)",
-                        "moe_bwd": "chain_bwd_kernel (fused MoE expert chains, backward)",
-                        "wgrad": "pgemm_x6_kernel+pgemm_reduce_kernel (weight gradients, bf16x6 MFMA)"})[rkind],
-            "class": rkind,
-            "class_ms_per_step": {k: round(v[0], 3) for k, v in kinds.items()},
-            "bound": "mfma",
-            "achieved": round(achieved, 3),
-            "peak": FP32_MFMA_PEAK_TFLOPS,
-            "unit": "TFLOP/s",
-            "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
-            "traffic": None if args.points else pmc_traffic(args.workload, rkind),
-            "avg_launch_us": round(avg_launch_ms * 1e3, 2),
-            "flops_per_launch": kflops / max(klaunch, 1),
-            "launches": klaunch,
-        },
+        "roofline": roofline(M0, args.dtype),
     }
+    if (args.dtype == "fp32" and not args.fp32_only and world == 1 and m["n_attn_hidden_dim"] == 256
+            and batches is None and not args.torch_adamw):
+        # BASELINE configs[2] names bf16 training: the same workload in the bf16 arithmetic mode, timed the
+        # same way on the same model and optimizer (the headline `value` above stays the fp32 path)
+        model.set_precision("bf16")
+        M1 = measure()
+        result["bf16_mode"] = {
+            "value": round(D["step_points"] * args.steps / M1["elapsed"], 1),
+            "ms_per_step": round(M1["elapsed"] / args.steps * 1e3, 4),
+            "dtype": "bf16",
+            "arithmetic": "one RNE bf16 operand per MFMA in the d=256 chains / projections / weight gradients, "
+                          "fp32 accumulation and storage (GNOT.set_precision('bf16'); tests/test_gpu_bf16.py: "
+                          "1e-2 of the fp64 oracle)",
+            "roofline": roofline(M1, "bf16"),
+        }
+        model.set_precision("fp32")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(w)
     if rank == 0:
