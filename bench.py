@@ -324,7 +324,7 @@ def main():
     it = {"k": 0}
     if shard:
         from gnot_amd import parallel as par
-        model.set_point_shard(par.PointShardComm())
+        model.set_point_shard(par.PointShardComm(stage_via_host=backend != "nccl"))
 
     # one training step = [forward + RelL2 + backward] -> (N>1: ONE all-reduce (sum) of the flat
     # gradient buffer) -> [AdamW].  With hipGraphs the two bracketed parts are captured once and
@@ -338,7 +338,7 @@ def main():
         out = model.forward_packed(x, x_off, theta, fns, fn_offs, n_global=D["n_global"])
         if shard:
             from gnot_amd import parallel as par
-            loss = par.rel_l2_loss_sharded(out, y, seg, B)
+            loss = par.rel_l2_loss_sharded(out, y, seg, B, stage_via_host=backend != "nccl")
         else:
             # native RelL2 (loss.py:14-23); mean over ALL samples of the step: local sum / global count
             loss = loss_fn(x_off, out, y) * (B / D["norm"])
