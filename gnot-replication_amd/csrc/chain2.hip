@@ -63,6 +63,12 @@ GNOT_DEV void c2f_layer(C2Pipe& pp, const u32x4* W, const u32x4 (&in)[KBI][NP], 
     for (int r = 0; r < 4; ++r) out[o][r] = GELU ? gelu(acc[r]) : acc[r];
     pin4(out[o]);
   };
+  // one part of tile o's epilogue (inside the next tile's MFMA stream): part 0 the save store
+  auto epi_part = [&](int o, const f32x4& acc, int r) {
+    if (SAVE && r == 0) buf_store_f32x4(make_float4(acc[0], acc[1], acc[2], acc[3]), rs, voff + 64 * o);
+    out[o][r] = GELU ? gelu(acc[r]) : acc[r];
+    asm volatile("" : "+v"(out[o][r]));
+  };
 #pragma unroll
   for (int o = 0; o < OT; ++o) {
     if (o == 0) c2_sync_n(pend0);
@@ -79,8 +85,14 @@ GNOT_DEV void c2f_layer(C2Pipe& pp, const u32x4* W, const u32x4 (&in)[KBI][NP], 
     }
     ++pp.cnt;
     const u32x4 bb = bias[4 * o + g];
-    const f32x4 acc = c2_tile<KBI, false, NP>(cb, in, __builtin_bit_cast(f32x4, bb), pp.lane);
-    if (o > 0) epi(o - 1, prev);
+    f32x4 acc;
+    if (o > 0) {
+      const f32x4 pv = prev;
+      acc = c2_tile_epi<KBI, NP>(cb, in, __builtin_bit_cast(f32x4, bb), pp.lane,
+                                 [&](int r) { epi_part(o - 1, pv, r); });
+    } else {
+      acc = c2_tile<KBI, false, NP>(cb, in, __builtin_bit_cast(f32x4, bb), pp.lane);
+    }
     prev = acc;
   }
   epi(OT - 1, prev);
@@ -188,6 +200,16 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP],
     buf_store_f32x4(make_float4(nx[o][0], nx[o][1], nx[o][2], nx[o][3]), rz, voff + 64 * o);
     pin4(nx[o]);
   };
+  // one part of tile o's epilogue (inside the next tile's MFMA stream): part 0 reads the saved
+  // pre-activation tile, part 3 stores dz
+  float4 hc;
+  auto epi_part = [&](int o, const f32x4& acc, int r) {
+    if (r == 0) hc = lds_read16_sync(slots + (o & 3) * 64 + pp.lane);
+    const float h = r == 0 ? hc.x : r == 1 ? hc.y : r == 2 ? hc.z : hc.w;
+    nx[o][r] = acc[r] * gelu_grad(h);
+    asm volatile("" : "+v"(nx[o][r]));
+    if (r == 3) buf_store_f32x4(make_float4(nx[o][0], nx[o][1], nx[o][2], nx[o][3]), rz, voff + 64 * o);
+  };
 #pragma unroll
   for (int o = 0; o < DT; ++o) {
     // ops after the weight DMA this wait retires (issued one tile earlier): the h tile requested with
@@ -202,8 +224,13 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP],
     ++pp.cnt;
     if (o + 2 < DT) dma16(rh, slots + ((o + 2) & 3) * 64, voff, 64 * (o + 2));
     else if (has_next_h) dma16(rh_next, slots + ((o + 2) & 3) * 64, voff, 64 * (o + 2 - DT));
-    const f32x4 acc = c2_tile<KBI, false, NP>(cb, in, f32x4{0.f, 0.f, 0.f, 0.f}, pp.lane);
-    if (o > 0) epi(o - 1, prev);
+    f32x4 acc;
+    if (o > 0) {
+      const f32x4 pv = prev;
+      acc = c2_tile_epi<KBI, NP>(cb, in, f32x4{0.f, 0.f, 0.f, 0.f}, pp.lane, [&](int r) { epi_part(o - 1, pv, r); });
+    } else {
+      acc = c2_tile<KBI, false, NP>(cb, in, f32x4{0.f, 0.f, 0.f, 0.f}, pp.lane);
+    }
     prev = acc;
     __builtin_amdgcn_sched_barrier(0);      // no code motion across tiles (register pressure)
   }

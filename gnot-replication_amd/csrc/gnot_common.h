@@ -368,6 +368,23 @@ GNOT_DEV void split8_np(const float (&v)[8], u32x4 (&p)[NP]) {
   else split8_bf16(v, p);
 }
 
+// the split of ONE element pair (elements 2d, 2d+1 of an 8-element group): dword d of every piece,
+// the same bits split8_np writes
+template <int NP>
+GNOT_DEV void split2_np(float v0, float v1, u32x4 (&p)[NP], int d) {
+  if constexpr (NP == 3) {
+    const unsigned a0 = f2u(v0), b0 = f2u(v1);
+    const float ra = v0 - u2f(a0 & 0xFFFF0000u), rb = v1 - u2f(b0 & 0xFFFF0000u);
+    const unsigned a1 = f2u(ra), b1 = f2u(rb);
+    const unsigned a2 = f2u(ra - u2f(a1 & 0xFFFF0000u)), b2 = f2u(rb - u2f(b1 & 0xFFFF0000u));
+    p[0][d] = (b0 & 0xFFFF0000u) | (a0 >> 16);
+    p[1][d] = (b1 & 0xFFFF0000u) | (a1 >> 16);
+    p[2][d] = (b2 & 0xFFFF0000u) | (a2 >> 16);
+  } else {
+    p[0][d] = (bf16_rne_bits(v1) << 16) | bf16_rne_bits(v0);
+  }
+}
+
 // B pieces of k-block t of the point-form activations in[KT][4]: bp[q] = 8 bf16 (4 dwords) of piece q
 template <int KT, int NP = 3>
 GNOT_DEV void split_block_x6(const float (&in)[KT][4], int t, u32x4 (&bp)[NP]) {

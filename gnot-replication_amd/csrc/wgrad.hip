@@ -370,7 +370,6 @@ constexpr int kWPiece = 8 * 64;                  // u32x4 per (operand, piece) i
 // one stage buffer: A pieces 0..NP-1 | B pieces 0..NP-1 (NP = 3: bf16x6, 1: bf16 mode)
 constexpr int w_buf(int np) { return 2 * np * kWPiece; }
 constexpr size_t w_lds_bytes(int np) { return 2 * (size_t)w_buf(np) * 16; }   // 96 KiB at NP = 3
-constexpr size_t kWLdsBytes = w_lds_bytes(3);
 
 GNOT_DEV void x6_mfma6(const u32x4 (&a)[3], const u32x4 (&b)[3], f32x16& c) {
 #define GNOT_MFMA32(X, Y) \
@@ -502,8 +501,100 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
   // V & 1: the first half of the waves (w and w + 4 share a SIMD) runs at raised issue priority, so
   //        after a barrier it gets through its MFMAs first and stages while its partner multiplies
   // V & 2: two raw register sets (the rows of stage s+2 in flight for two stages)
-  if ((V & 1) && wave < 4) __builtin_amdgcn_s_setprio(1);
-  if constexpr ((V & 2) == 0) {
+  // V & 4 (default): the staging of stage s+1 (GELU, split, LDS stores) and the row loads of stage s+2
+  //        are interleaved instruction by instruction with the MFMAs of stage s on the SAME wave, so
+  //        the VALU issues in the MFMA shadows instead of in a separate phase that both waves of a SIMD
+  //        reach together after every barrier (full 256 x 256 tiles; edge tiles take the plain loop)
+  if constexpr ((V & 4) != 0) {
+    if (pb >= pe) {
+      // empty split: the partials below are zero
+    } else {
+      Raw R;
+      load(R, pb);
+      stage(0, R);
+      load(R, pb + kWStage);
+      __syncthreads();
+      int buf = 0;
+      long p0 = pb;
+      // compute(buf) | stage(buf ^ 1, R) | load(R, pn) as ONE program order: after each six-MFMA
+      // group (one 32 x 32 block) comes one point's staging (mask, column sum, GELU; every second
+      // point the split of the pair just finished), then that point's row loads for stage pn.
+      // sched_barrier pins the order, so each wave alternates MFMA groups and VALU chunks and the two
+      // waves of a SIMD fill each other's gaps.
+      auto fused = [&](int b, long pn, auto GEL) {
+        const u32x4* A = wl + b * w_buf(NP);
+        const u32x4* Bm = A + NP * kWPiece;
+        u32x4 bf[2][NP], af[2][NP], pa[NP], pq[NP];
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+          for (int q = 0; q < NP; ++q) bf[jb][q] = Bm[q * kWPiece + (wc * 2 + jb) * 64 + lane];
+#pragma unroll
+        for (int q = 0; q < NP; ++q) af[0][q] = A[q * kWPiece + (wr * 4) * 64 + lane];
+        float ra[8], vb[8];
+        const unsigned pr = (unsigned)(pn + 8 * hw);
+        auto chunk = [&](int k) {
+          ra[k] = fa ? R.a[k] : 0.f;
+          dbacc += ra[k];
+          const float bv = fb ? R.b[k] : 0.f;
+          vb[k] = decltype(GEL)::value ? gelu(bv) : bv;
+          R.a[k] = buf_load_f32(rA, voA, (int)((pr + k) * (unsigned)J.lddz * 4u));
+          R.b[k] = buf_load_f32(rB, voB, (int)((pr + k) * (unsigned)J.ldx * 4u));
+          // pin the chunk's results here: IR-level sinking would otherwise move the whole staging
+          // next to its LDS stores after the last MFMA group (sched_barrier only binds the scheduler)
+          asm volatile("" : "+v"(ra[k]), "+v"(vb[k]), "+v"(dbacc));
+          if (k & 1) {
+            split2_np<NP>(ra[k - 1], ra[k], pa, k >> 1);
+            split2_np<NP>(vb[k - 1], vb[k], pq, k >> 1);
+#pragma unroll
+            for (int q = 0; q < NP; ++q) asm volatile("" : "+v"(pa[q][k >> 1]), "+v"(pq[q][k >> 1]));
+          }
+        };
+#pragma unroll
+        for (int ib = 0; ib < 4; ++ib) {
+          if (ib + 1 < 4) {
+#pragma unroll
+            for (int q = 0; q < NP; ++q) af[(ib + 1) & 1][q] = A[q * kWPiece + (wr * 4 + ib + 1) * 64 + lane];
+          }
+          mfma_np<NP>(af[ib & 1], bf[0], acc[ib][0]);
+          __builtin_amdgcn_sched_barrier(0);
+          chunk(2 * ib);
+          __builtin_amdgcn_sched_barrier(0);
+          mfma_np<NP>(af[ib & 1], bf[1], acc[ib][1]);
+          __builtin_amdgcn_sched_barrier(0);
+          chunk(2 * ib + 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        u32x4* base = wl + (b ^ 1) * w_buf(NP);
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {
+          base[q * kWPiece + sdst] = pa[q];
+          base[(NP + q) * kWPiece + sdst] = pq[q];
+        }
+      };
+      auto run = [&](auto GEL) {
+        for (; p0 + kWStage < pe; p0 += kWStage) {
+          fused(buf, p0 + 2 * kWStage, GEL);
+          __syncthreads();
+          buf ^= 1;
+        }
+      };
+      if (full) {
+        if (gel) run(std::true_type{});
+        else run(std::false_type{});
+      } else {
+        for (; p0 + kWStage < pe; p0 += kWStage) {
+          compute(buf);
+          stage(buf ^ 1, R);
+          load(R, p0 + 2 * kWStage);
+          __syncthreads();
+          buf ^= 1;
+        }
+      }
+      compute(buf);   // the last stage
+    }
+  } else if constexpr ((V & 2) == 0) {
+    if ((V & 1) && wave < 4) __builtin_amdgcn_s_setprio(1);
     Raw R;
     if (pb < pe) {
       load(R, pb);
@@ -522,6 +613,7 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
       buf ^= 1;
     }
   } else {
+    if ((V & 1) && wave < 4) __builtin_amdgcn_s_setprio(1);
     Raw R0, R1;
     if (pb < pe) {
       load(R0, pb);
@@ -621,32 +713,25 @@ hipError_t launch_wgrad(const WgradJob* jobs_dev, const int* wg_prefix_dev, int 
                         const int* red_prefix_dev, int total_red, float* slab, hipStream_t s, bool x6, bool wide,
                         int np) {
   if (njobs <= 0) return hipSuccess;
-  if (wide && np == 1) {
-    static bool attr1 = false;
-    if (!attr1) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(pgemm_x6w_kernel<0, 1>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)w_lds_bytes(1));
-      attr1 = true;
-    }
-    hipLaunchKernelGGL((pgemm_x6w_kernel<0, 1>), dim3(total_wgs), dim3(kWThreads), w_lds_bytes(1), s, jobs_dev,
-                       wg_prefix_dev, njobs, slab);
-  } else if (wide) {
-    // GNOT_X6W_VARIANT (diagnostics): bit 0 priority split, bit 1 two raw register sets
-    static const int var = std::getenv("GNOT_X6W_VARIANT") ? std::atoi(std::getenv("GNOT_X6W_VARIANT")) & 3 : 0;
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(pgemm_x6w_kernel<0>), hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWLdsBytes);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(pgemm_x6w_kernel<1>), hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWLdsBytes);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(pgemm_x6w_kernel<2>), hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWLdsBytes);
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(pgemm_x6w_kernel<3>), hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWLdsBytes);
-      attr = true;
-    }
-    switch (var) {
-#define GNOT_X6W(V_) \
-  case V_: hipLaunchKernelGGL(pgemm_x6w_kernel<V_>, dim3(total_wgs), dim3(kWThreads), kWLdsBytes, s, jobs_dev, wg_prefix_dev, njobs, slab); break;
-      GNOT_X6W(0) GNOT_X6W(1) GNOT_X6W(2) GNOT_X6W(3)
+  if (wide) {
+    // GNOT_X6W_VARIANT (diagnostics): 4 (default) staging interleaved with the MFMAs; 0 the plain
+    // double-buffered loop; 1 / 2 / 3 its priority-split / two-register-set forms (x6 only)
+    static const int var = std::getenv("GNOT_X6W_VARIANT") ? std::atoi(std::getenv("GNOT_X6W_VARIANT")) & 7 : 4;
+    const int v = np == 1 ? (var & 4) : var;
+    const size_t lds = w_lds_bytes(np);
+#define GNOT_X6W(V_, NP_)                                                                                      \
+  if (v == V_ && np == NP_) {                                                                                  \
+    static bool attr = false;                                                                                  \
+    if (!attr) {                                                                                               \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(pgemm_x6w_kernel<V_, NP_>),                      \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                         \
+      attr = true;                                                                                             \
+    }                                                                                                          \
+    hipLaunchKernelGGL((pgemm_x6w_kernel<V_, NP_>), dim3(total_wgs), dim3(kWThreads), lds, s, jobs_dev,         \
+                       wg_prefix_dev, njobs, slab);                                                            \
+  }
+    GNOT_X6W(0, 3) GNOT_X6W(1, 3) GNOT_X6W(2, 3) GNOT_X6W(3, 3) GNOT_X6W(4, 3) GNOT_X6W(0, 1) GNOT_X6W(4, 1)
 #undef GNOT_X6W
-    }
   } else if (x6)
     hipLaunchKernelGGL(pgemm_x6_kernel, dim3(total_wgs), dim3(256), 0, s, jobs_dev, wg_prefix_dev, njobs, slab);
   else

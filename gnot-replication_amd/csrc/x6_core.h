@@ -46,6 +46,37 @@ GNOT_DEV f32x4 c2_tile(const u32x4* __restrict__ cb, const u32x4 (&bp)[KB][NP], 
   return acc;
 }
 
+// c2_tile with the previous tile's epilogue split into 4 parts, part i placed after the MFMAs of k-block
+// 2i+1 (the rest after the last block when KB < 8).  sched_barrier pins the order for the scheduler and
+// the epilogue pins its results with empty asm (IR sinking would otherwise move them to their uses), so
+// the VALU issues in this wave's own MFMA shadows instead of as one burst after the tile that both
+// waves of a SIMD reach together.
+template <int KB, int NP, typename Epi>
+GNOT_DEV f32x4 c2_tile_epi(const u32x4* __restrict__ cb, const u32x4 (&bp)[KB][NP], f32x4 acc, int lane, Epi&& epi) {
+  u32x4 a[NP];
+#pragma unroll
+  for (int t = 0; t < KB; ++t) {
+#pragma unroll
+    for (int q = 0; q < NP; ++q) a[q] = cb[(t * NP + q) * WAVE + lane];
+    if constexpr (NP == 3) {
+      acc = mfma_bf16(a[2], bp[t][0], acc);
+      acc = mfma_bf16(a[1], bp[t][1], acc);
+      acc = mfma_bf16(a[0], bp[t][2], acc);
+      acc = mfma_bf16(a[1], bp[t][0], acc);
+      acc = mfma_bf16(a[0], bp[t][1], acc);
+    }
+    acc = mfma_bf16(a[0], bp[t][0], acc);
+    if ((t & 1) && (t >> 1) < 4) {
+      __builtin_amdgcn_sched_barrier(0);
+      epi(t >> 1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+#pragma unroll
+  for (int i = KB / 2; i < 4; ++i) epi(i);
+  return acc;
+}
+
 // The weight stream of one workgroup: chunk = one output tile.  `begin` waits for the chunk in flight,
 // barriers, and starts the DMA of the following chunk (tile o+1 of this image, or `next` = the first
 // tile of the next image, or nothing).
