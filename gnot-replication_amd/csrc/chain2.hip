@@ -22,6 +22,13 @@
 #include "gnot_kernels.h"
 #include "x6_core.h"
 
+#ifndef GNOT_C2_AHEAD_F
+#define GNOT_C2_AHEAD_F true
+#endif
+#ifndef GNOT_C2_AHEAD_B
+#define GNOT_C2_AHEAD_B true
+#endif
+
 namespace gnot {
 
 // LDS of one workgroup (u32x4 units): two weight-chunk buffers, two 1 KiB bias buffers (layer parity,
@@ -34,14 +41,6 @@ struct C2Lds {
   static constexpr int kBytes = (kHs + kC2Waves * 4 * 64) * 16;
 };
 
-struct C2Pipe {
-  u32x4* lds;
-  int WB;
-  int cnt;          // weight chunks consumed (buffer parity)
-  int wave, lane;
-  GNOT_DEV const u32x4* cur() const { return lds + (cnt & 1) * WB; }
-  GNOT_DEV u32x4* nxt() const { return lds + ((cnt + 1) & 1) * WB; }
-};
 
 // ------------------------------------------------------------------------------------------ forward
 // One forward layer: OT output tiles h = W a + b of the split input `in`; saves h (SAVE) and returns
@@ -88,8 +87,8 @@ GNOT_DEV void c2f_layer(C2Pipe& pp, const u32x4* W, const u32x4 (&in)[KBI][NP], 
     f32x4 acc;
     if (o > 0) {
       const f32x4 pv = prev;
-      acc = c2_tile_epi<KBI, NP>(cb, in, __builtin_bit_cast(f32x4, bb), pp.lane,
-                                 [&](int r) { epi_part(o - 1, pv, r); });
+      auto ep = [&](int r) { epi_part(o - 1, pv, r); };
+      acc = c2_tile_epi<KBI, NP, GNOT_C2_AHEAD_F>(cb, in, __builtin_bit_cast(f32x4, bb), pp.lane, ep);
     } else {
       acc = c2_tile<KBI, false, NP>(cb, in, __builtin_bit_cast(f32x4, bb), pp.lane);
     }
@@ -227,7 +226,8 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP],
     f32x4 acc;
     if (o > 0) {
       const f32x4 pv = prev;
-      acc = c2_tile_epi<KBI, NP>(cb, in, f32x4{0.f, 0.f, 0.f, 0.f}, pp.lane, [&](int r) { epi_part(o - 1, pv, r); });
+      auto ep = [&](int r) { epi_part(o - 1, pv, r); };
+      acc = c2_tile_epi<KBI, NP, GNOT_C2_AHEAD_B>(cb, in, f32x4{0.f, 0.f, 0.f, 0.f}, pp.lane, ep);
     } else {
       acc = c2_tile<KBI, false, NP>(cb, in, f32x4{0.f, 0.f, 0.f, 0.f}, pp.lane);
     }

@@ -42,6 +42,10 @@ GNOT_DEV f32x4 c2_tile(const u32x4* __restrict__ cb, const u32x4 (&bp)[KB][NP], 
       acc = mfma_bf16(w[0], bp[t][1], acc);
     }
     acc = mfma_bf16(w[0], bp[t][0], acc);
+    if (AHEAD) {
+      if (t + 1 < KB) __builtin_amdgcn_sched_group_barrier(0x100, NP, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, NP == 3 ? 6 : 1, 0);
+    }
   }
   return acc;
 }
@@ -51,13 +55,25 @@ GNOT_DEV f32x4 c2_tile(const u32x4* __restrict__ cb, const u32x4 (&bp)[KB][NP], 
 // the epilogue pins its results with empty asm (IR sinking would otherwise move them to their uses), so
 // the VALU issues in this wave's own MFMA shadows instead of as one burst after the tile that both
 // waves of a SIMD reach together.
-template <int KB, int NP, typename Epi>
+template <int KB, int NP, bool AHEAD, typename Epi>
 GNOT_DEV f32x4 c2_tile_epi(const u32x4* __restrict__ cb, const u32x4 (&bp)[KB][NP], f32x4 acc, int lane, Epi&& epi) {
-  u32x4 a[NP];
+  u32x4 ab[AHEAD ? 2 : 1][NP];
+  if (AHEAD) {
+#pragma unroll
+    for (int q = 0; q < NP; ++q) ab[0][q] = cb[q * WAVE + lane];
+  }
 #pragma unroll
   for (int t = 0; t < KB; ++t) {
+    if (AHEAD) {
+      if (t + 1 < KB) {
 #pragma unroll
-    for (int q = 0; q < NP; ++q) a[q] = cb[(t * NP + q) * WAVE + lane];
+        for (int q = 0; q < NP; ++q) ab[(t + 1) & 1][q] = cb[((t + 1) * NP + q) * WAVE + lane];
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < NP; ++q) ab[0][q] = cb[(t * NP + q) * WAVE + lane];
+    }
+    const u32x4(&a)[NP] = ab[AHEAD ? (t & 1) : 0];
     if constexpr (NP == 3) {
       acc = mfma_bf16(a[2], bp[t][0], acc);
       acc = mfma_bf16(a[1], bp[t][1], acc);
@@ -66,6 +82,12 @@ GNOT_DEV f32x4 c2_tile_epi(const u32x4* __restrict__ cb, const u32x4 (&bp)[KB][N
       acc = mfma_bf16(a[0], bp[t][1], acc);
     }
     acc = mfma_bf16(a[0], bp[t][0], acc);
+    if (AHEAD) {
+      // keep block t+1's fragment reads ahead of block t's MFMAs (the scheduler otherwise sinks them
+      // next to their use to save registers, exposing the LDS latency every block)
+      if (t + 1 < KB) __builtin_amdgcn_sched_group_barrier(0x100, NP, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, NP == 3 ? 6 : 1, 0);
+    }
     if ((t & 1) && (t >> 1) < 4) {
       __builtin_amdgcn_sched_barrier(0);
       epi(t >> 1);
@@ -120,12 +142,25 @@ GNOT_DEV void c2_sync_n(int n) {   // n is wave-uniform and small
   n = 0;
 #endif
   switch (n) {
-    case 0: c2_sync<0>(); break;
     case 1: c2_sync<1>(); break;
     case 2: c2_sync<2>(); break;
-    default: c2_sync<3>(); break;
+    case 3: c2_sync<3>(); break;
+    case 4: c2_sync<4>(); break;
+    case 5: c2_sync<5>(); break;
+    case 6: c2_sync<6>(); break;
+    default: c2_sync<0>(); break;
   }
 }
+// the double-buffered weight-chunk stream of a chain kernel (chain2.hip)
+struct C2Pipe {
+  u32x4* lds;
+  int WB;
+  int cnt;          // weight chunks consumed (buffer parity)
+  int wave, lane;
+  GNOT_DEV const u32x4* cur() const { return lds + (cnt & 1) * WB; }
+  GNOT_DEV u32x4* nxt() const { return lds + ((cnt + 1) & 1) * WB; }
+};
+
 // LDS read of a slot this wave filled by LDS-DMA and already waited for with a counted vmcnt: inline
 // asm, so hipcc does not insert its own vmcnt(0) for the DMA still in flight to OTHER buffers (it cannot
 // tell the addresses apart and would drain the whole pipeline)
