@@ -103,7 +103,7 @@ def rel_l2_loss(out, tgt, seg, B):
     return (num / den).sqrt().mean()
 
 
-def make_rank_batch(w, rank, world, device):
+def make_rank_batch(w, rank, world, device, force_shard=False):
     """This rank's share of the step's data, the loss normaliser and the step's total point count.
     sample-DP: `B` meshes of `N` points per rank (seeded by rank); configs[4]: the rank's LPT share of
     64 variable meshes; point-shard (configs[3]): the rank's slice of ONE mesh (every rank generates
@@ -133,13 +133,14 @@ def make_rank_batch(w, rank, world, device):
         return dict(x=to(torch.cat(xs)), x_off=x_off, theta=to(torch.cat(th)), fns=[to(f) for f in fns],
                     fn_offs=fn_offs, y=to(torch.cat(ys)), seg=to(seg), B=Bl, norm=w["B"], n_global=None,
                     step_points=sum(sizes), mesh_points=f"{min(sizes)}..{max(sizes)}", meshes=w["B"])
-    if w.get("shard") or (w.get("shard_weak") and world > 1):
+    if w.get("shard") or (w.get("shard_weak") and (world > 1 or force_shard)):
         w = dict(w, N=w["N"] * (world if w.get("shard_weak") else 1))     # weak: N points per rank
         x, x_off, theta, fns, fn_offs, y, seg = make_batch(w, 100, torch.device("cpu"))
         lo, hi = par.shard_range(w["N"], rank, world)
         to = lambda t: t.to(device)
         return dict(x=to(x[lo:hi]), x_off=[0, hi - lo], theta=to(theta), fns=[to(f) for f in fns], fn_offs=fn_offs,
-                    y=to(y[lo:hi]), seg=to(seg[lo:hi]), B=1, norm=1, n_global=[w["N"]] if world > 1 else None,
+                    y=to(y[lo:hi]), seg=to(seg[lo:hi]), B=1, norm=1,
+                    n_global=[w["N"]] if (world > 1 or force_shard) else None,
                     step_points=w["N"],
                     mesh_points=f"{w['N']:,} ({hi - lo:,} on this GPU)", meshes=1)
     x, x_off, theta, fns, fn_offs, y, seg = make_batch(w, 100 + rank, device)
@@ -262,8 +263,14 @@ def main():
     backend = os.environ.get("GNOT_BENCH_BACKEND", "nccl")
     if os.environ.get("GNOT_BENCH_ONE_GPU"):
         local = 0
-    if world > 1:
+    # GNOT_BENCH_FORCE_SHARD=1: run the point-shard path (eager, engine callbacks, RCCL collectives) even
+    # at one rank -- the N=1 reference of the sharded step the multi-GPU runs take
+    force_shard = os.environ.get("GNOT_BENCH_FORCE_SHARD") == "1"
+    if world > 1 or force_shard:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -283,7 +290,7 @@ def main():
     model = GNOT(*[m[k] for k in ("input_dim", "theta_dim", "input_func_dim", "out_dim", "n_attn_layers",
                                   "n_attn_hidden_dim", "n_mlp_num_layers", "n_mlp_hidden_dim",
                                   "n_input_hidden_dim", "n_expert", "n_head", "n_input_functions")]).to(device)
-    shard = bool(w.get("shard") or w.get("shard_weak")) and world > 1
+    shard = bool(w.get("shard") or w.get("shard_weak")) and (world > 1 or force_shard)
     # the point-shard exchanges run inside the engine's launch sequence (RCCL through callbacks): eager
     use_graph = not args.no_graph and not shard
     from gnot_amd import train as gtrain
@@ -294,7 +301,7 @@ def main():
     else:
         opt = gtrain.FlatAdamW(gtrain.flatten_parameters(model), lr=1e-3)
     loss_fn = gtrain.RelL2Loss()
-    D = make_rank_batch(w, rank, world, device)
+    D = make_rank_batch(w, rank, world, device, force_shard)
     x, x_off, theta, fns, fn_offs, y, seg, B = (D[k] for k in ("x", "x_off", "theta", "fns", "fn_offs", "y", "seg", "B"))
     eng = model.engine()
     eng.param_grads = bool(args.torch_adamw)      # the native AdamW reads the gradient arena directly
@@ -496,7 +503,7 @@ def main():
                    "input_functions": m["n_input_functions"],
                    "geometry": "new mesh order every step (--vary-geometry)" if batches is not None else "fixed",
                    "moe_recompute": recompute,
-                   "parallelism": (f"point-shard{world}" if shard else f"sample-dp{world}") if world > 1 else "single",
+                   "parallelism": (f"point-shard{world}" if shard else f"sample-dp{world}") if (world > 1 or shard) else "single",
                    "step": "pack+fwd+RelL2+bwd+AdamW (native loss, " + ("torch fused AdamW" if args.torch_adamw else "native flat AdamW") + ")" + (" (hipGraph replay)" if use_graph else " (eager)")},
         "roofline": roofline(M0, args.dtype),
     }
@@ -520,7 +527,7 @@ def main():
         result["cpu_baseline"] = cpu_baseline(w)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

@@ -48,10 +48,14 @@ def _case(cfg, Ns, Ms, seed):
     return fx
 
 
-def _rank(rank, world, port, cfg, Ns, Ms, q):
+def _rank(rank, world, port, cfg, Ns, Ms, q, backend="gloo"):
     sys.path[:0] = [ROOT, os.path.join(ROOT, "gnot-replication_amd"), os.path.join(ROOT, "tests")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from golden_util import check_parity, model_args
         from gnot_amd import GNOT
@@ -60,7 +64,7 @@ def _rank(rank, world, port, cfg, Ns, Ms, q):
         dev = torch.device("cuda", 0)
         m = GNOT(*model_args(cfg)).to(dev)
         m.load_state_dict({k: torch.from_numpy(v).float() for k, v in fx["params"].items()})
-        m.set_point_shard(par.PointShardComm(stage_via_host=True))
+        m.set_point_shard(par.PointShardComm(stage_via_host=backend != "nccl"))
         loc_off, ranges = par.shard_offsets(Ns, rank, world)
         rows = np.concatenate([np.arange(fx["x_off"][b] + lo, fx["x_off"][b] + hi) for b, (lo, hi) in enumerate(ranges)])
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).float().to(dev)
@@ -68,9 +72,12 @@ def _rank(rank, world, port, cfg, Ns, Ms, q):
                                [o.tolist() for o in fx["fn_offs"]], n_global=Ns)
         (out * t(fx["G"][rows])).sum().backward()
         flat = m.engine().grad_flat
-        h = flat.cpu()
-        dist.all_reduce(h)                     # parameter gradients: sum over ranks
-        flat.copy_(h.to(dev))
+        if backend == "nccl":
+            dist.all_reduce(flat)              # parameter gradients: sum over ranks (RCCL)
+        else:
+            h = flat.cpu()
+            dist.all_reduce(h)                 # parameter gradients: sum over ranks
+            flat.copy_(h.to(dev))
         torch.cuda.synchronize()
         outs = [None] * world
         dist.all_gather_object(outs, (rows, out.detach().double().cpu().numpy()))
@@ -111,4 +118,22 @@ def test_point_sharded_gnot_matches_oracle(world, case):
     for p in procs:
         p.join(timeout=30)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert not errs, errs
+
+
+def test_point_sharded_gnot_rccl_path():
+    """The RCCL branch of PointShardComm (collectives issued on the engine's stream through a torch
+    ExternalStream, no host staging) at world size 1 -- the only RCCL world a one-GPU box can form: the
+    state all-reduces and scramble all-to-alls run through RCCL on device buffers, the result must still
+    match the oracle.  (N > 1 ranks over RCCL runs in the driver's multi-GPU bench.)"""
+    case = dict(cfg=dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=2, n_attn_layers=2, d=64,
+                         n_mlp_num_layers=2, n_expert=3, n_head=8, n_input_functions=1),
+                Ns=[150, 97], Ms=[[40, 31]])
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rank, args=(0, 1, _free_port(), case["cfg"], case["Ns"], case["Ms"], q, "nccl"))
+    p.start()
+    errs = q.get(timeout=100)
+    p.join(timeout=30)
+    assert p.exitcode == 0, p.exitcode
     assert not errs, errs
