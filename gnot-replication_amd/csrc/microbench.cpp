@@ -204,6 +204,21 @@ int main(int argc, char** argv) {
         for (size_t i = 0; i < ndw; ++i) { n2 += (got[i] - ref[i]) * (double)(got[i] - ref[i]); d2 += (double)ref[i] * ref[i]; }
         std::printf("wgrad MoE  bf16 wide 256x256 (%d WGs):    %8.2f us  %6.1f TFLOP/s  (rel-L2 vs fp32 %.2e)\n",
                     njobs * splits, t, fl / t / 1e6, std::sqrt(n2 / (d2 + 1e-30)));
+        if (wgs == 512) {
+          // diagnostics of the wide x6 kernel: without the GELU of the B operand, with every point
+          // reading row 0 (L2-resident rows: no HBM latency), and both
+          const char* what[3] = {"no-GELU operand", "L2-resident rows", "no-GELU + L2 rows"};
+          for (int v = 0; v < 3; ++v) {
+            std::vector<WgradJob> dj(wj);
+            for (auto& J : dj) {
+              if (v != 1) J.x_gelu = 0;
+              if (v != 0) { J.lddz = 0; J.ldx = 0; }
+            }
+            CK(hipMemcpy(dwj, dj.data(), dj.size() * sizeof(WgradJob), hipMemcpyHostToDevice));
+            t = time_us([&] { CK(launch_wgrad(dwj, dwpre, njobs, njobs * splits, dwpre + njobs, red, wslab, nullptr, true, true)); }, 20);
+            std::printf("wgrad MoE  bf16x6 wide, %-18s   %8.2f us  %6.1f TFLOP/s\n", what[v], t, fl / t / 1e6);
+          }
+        }
         CK(hipFree(dwj));
         CK(hipFree(dwpre));
         CK(hipFree(wslab));
