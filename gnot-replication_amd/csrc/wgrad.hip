@@ -501,99 +501,11 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
   // V & 1: the first half of the waves (w and w + 4 share a SIMD) runs at raised issue priority, so
   //        after a barrier it gets through its MFMAs first and stages while its partner multiplies
   // V & 2: two raw register sets (the rows of stage s+2 in flight for two stages)
-  // V & 4: the staging of stage s+1 (GELU, split, LDS stores) and the row loads of stage s+2
+  // V & 4 (default): the staging of stage s+1 (GELU, split, LDS stores) and the row loads of stage s+2
   //        are interleaved instruction by instruction with the MFMAs of stage s on the SAME wave, so
   //        the VALU issues in the MFMA shadows instead of in a separate phase that both waves of a SIMD
   //        reach together after every barrier (full 256 x 256 tiles; edge tiles take the plain loop)
-  if constexpr ((V & 8) != 0) {
-    // V & 8 (default): the interleaved loop of V & 4 over THREE stage buffers (144 KiB at x6).  The
-    // staging writes two stages ahead, so the buffer of the NEXT stage is complete (and visible) one
-    // barrier earlier: its first fragments (B blocks, A block 0) are read before the barrier that ends
-    // the current stage, and the next stage's MFMAs start right after it instead of behind a burst of
-    // nine fragment reads per wave.
-    if (pb < pe) {
-      Raw R;
-      auto bufp = [&](int b) { return wl + b * w_buf(NP); };
-      {
-        // every job takes this path: features past out / in are staged as zeros (the stores below skip
-        // them), so a narrow job costs a full tile of MFMAs but the loop stays one straight-line body
-        auto read_first = [&](const u32x4* A, u32x4 (&bf)[2][NP], u32x4 (&af0)[NP]) {
-          const u32x4* Bm = A + NP * kWPiece;
-#pragma unroll
-          for (int jb = 0; jb < 2; ++jb)
-#pragma unroll
-            for (int q = 0; q < NP; ++q) bf[jb][q] = Bm[q * kWPiece + (wc * 2 + jb) * 64 + lane];
-#pragma unroll
-          for (int q = 0; q < NP; ++q) af0[q] = A[q * kWPiece + (wr * 4) * 64 + lane];
-        };
-        auto run3 = [&](auto GEL) {
-          // prologue: stages pb and pb+16 into buffers 0 and 1 (a stage past pe is staged as zeros)
-          load(R, pb);
-          stage_v(0, R, GEL);
-          load(R, pb + kWStage);
-          {
-            const float keep = dbacc;
-            stage_v(1, R, GEL);
-            if (pb + kWStage >= pe) dbacc = keep;
-          }
-          load(R, pb + 2 * kWStage);
-          __syncthreads();
-          u32x4 bf[2][NP], af[2][NP];
-          read_first(bufp(0), bf, af[0]);
-          int cb = 0;
-          for (long p0 = pb; p0 < pe; p0 += kWStage) {
-            const u32x4* A = bufp(cb);
-            const bool live = p0 + 2 * kWStage < pe;     // the stage staged here is inside the split
-            const unsigned pr = (unsigned)(p0 + 3 * kWStage + 8 * hw);
-            float ra[8], vb[8];
-            u32x4 pa[NP], pq[NP];
-            auto chunk = [&](int k) {
-              ra[k] = (fa && live) ? R.a[k] : 0.f;
-              dbacc += ra[k];
-              const float bv = fb ? R.b[k] : 0.f;
-              vb[k] = decltype(GEL)::value ? gelu(bv) : bv;
-              R.a[k] = buf_load_f32(rA, voA, (int)((pr + k) * (unsigned)J.lddz * 4u));
-              R.b[k] = buf_load_f32(rB, voB, (int)((pr + k) * (unsigned)J.ldx * 4u));
-              asm volatile("" : "+v"(ra[k]), "+v"(vb[k]), "+v"(dbacc));
-              if (k & 1) {
-                split2_np<NP>(ra[k - 1], ra[k], pa, k >> 1);
-                split2_np<NP>(vb[k - 1], vb[k], pq, k >> 1);
-#pragma unroll
-                for (int q = 0; q < NP; ++q) asm volatile("" : "+v"(pa[q][k >> 1]), "+v"(pq[q][k >> 1]));
-              }
-            };
-#pragma unroll
-            for (int ib = 0; ib < 4; ++ib) {
-              if (ib + 1 < 4) {
-#pragma unroll
-                for (int q = 0; q < NP; ++q) af[(ib + 1) & 1][q] = A[q * kWPiece + (wr * 4 + ib + 1) * 64 + lane];
-              }
-              mfma_np<NP>(af[ib & 1], bf[0], acc[ib][0]);
-              __builtin_amdgcn_sched_barrier(0);
-              chunk(2 * ib);
-              __builtin_amdgcn_sched_barrier(0);
-              mfma_np<NP>(af[ib & 1], bf[1], acc[ib][1]);
-              __builtin_amdgcn_sched_barrier(0);
-              chunk(2 * ib + 1);
-              __builtin_amdgcn_sched_barrier(0);
-            }
-            const int tb = cb == 0 ? 2 : cb - 1;          // (cb + 2) % 3: two stages ahead
-            u32x4* base = bufp(tb);
-#pragma unroll
-            for (int q = 0; q < NP; ++q) {
-              base[q * kWPiece + sdst] = pa[q];
-              base[(NP + q) * kWPiece + sdst] = pq[q];
-            }
-            cb = cb == 2 ? 0 : cb + 1;
-            if (p0 + kWStage < pe) read_first(bufp(cb), bf, af[0]);   // written one stage ago
-            __syncthreads();
-          }
-        };
-        if (gel) run3(std::true_type{});
-        else run3(std::false_type{});
-      }
-    }
-  } else if constexpr ((V & 4) != 0) {
+  if constexpr ((V & 4) != 0) {
     if (pb >= pe) {
       // empty split: the partials below are zero
     } else {
@@ -802,12 +714,11 @@ hipError_t launch_wgrad(const WgradJob* jobs_dev, const int* wg_prefix_dev, int 
                         int np) {
   if (njobs <= 0) return hipSuccess;
   if (wide) {
-    // GNOT_X6W_VARIANT (diagnostics): 8 (default) interleaved staging over three stage buffers; 4 the
-    // same over two; 0 the plain double-buffered loop; 1 / 2 / 3 its priority-split / two-register-set
+    // GNOT_X6W_VARIANT (diagnostics): 4 (default) staging interleaved with the MFMAs; 0 the plain double-buffered loop; 1 / 2 / 3 its priority-split / two-register-set
     // forms (x6 only)
-    static const int var = std::getenv("GNOT_X6W_VARIANT") ? std::atoi(std::getenv("GNOT_X6W_VARIANT")) & 15 : 8;
-    const int v = np == 1 ? (var & 12) : var;
-    const size_t lds = (v & 8) ? 3 * (size_t)w_buf(np) * 16 : w_lds_bytes(np);
+    static const int var = std::getenv("GNOT_X6W_VARIANT") ? std::atoi(std::getenv("GNOT_X6W_VARIANT")) & 7 : 4;
+    const int v = np == 1 ? (var & 4) : var;
+    const size_t lds = w_lds_bytes(np);
 #define GNOT_X6W(V_, NP_)                                                                                      \
   if (v == V_ && np == NP_) {                                                                                  \
     static bool attr = false;                                                                                  \
@@ -819,8 +730,7 @@ hipError_t launch_wgrad(const WgradJob* jobs_dev, const int* wg_prefix_dev, int 
     hipLaunchKernelGGL((pgemm_x6w_kernel<V_, NP_>), dim3(total_wgs), dim3(kWThreads), lds, s, jobs_dev,         \
                        wg_prefix_dev, njobs, slab);                                                            \
   }
-    GNOT_X6W(0, 3) GNOT_X6W(1, 3) GNOT_X6W(2, 3) GNOT_X6W(3, 3) GNOT_X6W(4, 3) GNOT_X6W(8, 3)
-    GNOT_X6W(0, 1) GNOT_X6W(4, 1) GNOT_X6W(8, 1)
+    GNOT_X6W(0, 3) GNOT_X6W(1, 3) GNOT_X6W(2, 3) GNOT_X6W(3, 3) GNOT_X6W(4, 3) GNOT_X6W(0, 1) GNOT_X6W(4, 1)
 #undef GNOT_X6W
   } else if (x6)
     hipLaunchKernelGGL(pgemm_x6_kernel, dim3(total_wgs), dim3(256), 0, s, jobs_dev, wg_prefix_dev, njobs, slab);
