@@ -201,11 +201,11 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP],
   };
   // one part of tile o's epilogue (inside the next tile's MFMA stream): part 0 reads the saved
   // pre-activation tile, part 3 stores dz
-  float4 hc;
+  f32x4 hc;
   auto epi_part = [&](int o, const f32x4& acc, int r) {
-    if (r == 0) hc = lds_read16_sync(slots + (o & 3) * 64 + pp.lane);
-    const float h = r == 0 ? hc.x : r == 1 ? hc.y : r == 2 ? hc.z : hc.w;
-    nx[o][r] = acc[r] * gelu_grad(h);
+    // the saved tile was read at the top of this tile (lds_read16_issue); wait for it here
+    if (r == 0) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(hc) :: "memory");
+    nx[o][r] = acc[r] * gelu_grad(hc[r]);
     asm volatile("" : "+v"(nx[o][r]));
     if (r == 3) buf_store_f32x4(make_float4(nx[o][0], nx[o][1], nx[o][2], nx[o][3]), rz, voff + 64 * o);
   };
@@ -225,6 +225,9 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP],
     else if (has_next_h) dma16(rh_next, slots + ((o + 2) & 3) * 64, voff, 64 * (o + 2 - DT));
     f32x4 acc;
     if (o > 0) {
+      // the saved h tile of the epilogue below, read now so its LDS latency hides behind the first
+      // k-blocks' MFMAs (its DMA, three tiles back, was retired by the counted wait above)
+      hc = lds_read16_issue(slots + ((o - 1) & 3) * 64 + pp.lane);
       const f32x4 pv = prev;
       auto ep = [&](int r) { epi_part(o - 1, pv, r); };
       acc = c2_tile_epi<KBI, NP, GNOT_C2_AHEAD_B>(cb, in, f32x4{0.f, 0.f, 0.f, 0.f}, pp.lane, ep);

@@ -170,6 +170,15 @@ GNOT_DEV float4 lds_read16_sync(const u32x4* p) {
   asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
   return v;
 }
+// the same read WITHOUT the wait: the result registers are valid only after a later
+// `s_waitcnt lgkmcnt(0)` asm that names them as in/out operands (so the compiler does not touch them
+// in between); an LDS op older than the compiler's own only makes its counted waits stricter
+GNOT_DEV f32x4 lds_read16_issue(const u32x4* p) {
+  f32x4 v;
+  const unsigned a = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) u32x4*)p;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
 // this wave's own LDS-DMA (lane l: 16 B at lds + l) from a buffer resource at byte offset voff + soff
 GNOT_DEV void dma16(rsrc_t r, u32x4* lds, int voff, int soff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void_ptr)lds, 16, voff, soff, 0, 0);
