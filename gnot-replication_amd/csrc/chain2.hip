@@ -190,39 +190,45 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP],
   constexpr int DT = 16, TU = c2_tile_u4(KBI, NP);
   u32x4* slots = pp.lds + C2Lds<256, NP>::kHs + pp.wave * 4 * 64;
   f32x4 prev;
-  auto epi = [&](int o, const f32x4& acc) {
-    const float4 hc = lds_read16_sync(slots + (o & 3) * 64 + pp.lane);
-    nx[o][0] = acc[0] * gelu_grad(hc.x);
-    nx[o][1] = acc[1] * gelu_grad(hc.y);
-    nx[o][2] = acc[2] * gelu_grad(hc.z);
-    nx[o][3] = acc[3] * gelu_grad(hc.w);
-    buf_store_f32x4(make_float4(nx[o][0], nx[o][1], nx[o][2], nx[o][3]), rz, voff + 64 * o);
-    pin4(nx[o]);
-  };
-  // one part of tile o's epilogue (inside the next tile's MFMA stream): part 0 reads the saved
-  // pre-activation tile, part 3 stores dz
+  // one part of tile o's epilogue (inside the next tile's MFMA stream): part 0 waits for the saved
+  // pre-activation tile
   f32x4 hc;
+  float gh[DT][4];
   auto epi_part = [&](int o, const f32x4& acc, int r) {
     // the saved tile was read at the top of this tile (lds_read16_issue); wait for it here
     if (r == 0) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(hc) :: "memory");
-    nx[o][r] = acc[r] * gelu_grad(hc[r]);
+    float Phi, e;
+    gelu_parts(hc[r], Phi, e);
+    nx[o][r] = acc[r] * fmaf(hc[r] * kInvSqrt2Pi, e, Phi);
     asm volatile("" : "+v"(nx[o][r]));
-    if (r == 3) buf_store_f32x4(make_float4(nx[o][0], nx[o][1], nx[o][2], nx[o][3]), rz, voff + 64 * o);
+    if (kChainGeluInPlace) {
+      // gelu(h) = h Phi from the same erf replaces h in the save (the weight gradients' B operand,
+      // read after this kernel; nothing else reads h later)
+      gh[o][r] = hc[r] * Phi;
+      asm volatile("" : "+v"(gh[o][r]));
+    }
   };
+  // tile o's stores (dz, and gelu(h) in place) are issued at the top of tile o+2, after that tile's
+  // DMAs: a counted wait only retires the ops issued before the DMA it waits for, so each store gets
+  // two tiles to drain instead of one
+  auto stores = [&](int o) {
+    buf_store_f32x4(make_float4(nx[o][0], nx[o][1], nx[o][2], nx[o][3]), rz, voff + 64 * o);
+    if (kChainGeluInPlace) buf_store_f32x4(make_float4(gh[o][0], gh[o][1], gh[o][2], gh[o][3]), rh, voff + 64 * o);
+  };
+  constexpr int S = kChainGeluInPlace ? 2 : 1;          // stores per tile
 #pragma unroll
   for (int o = 0; o < DT; ++o) {
-    // ops after the weight DMA this wait retires (issued one tile earlier): the h tile requested with
-    // it (none when that request would have been past the next layer) and the dz store of tile o-2
+    // ops issued after the weight DMA this wait retires (at the top of tile o-1): that tile's h DMA
+    // (none when it would be past the next layer) and the stores of tile o-3
     if (o == 0) c2_sync_n(pend0);
-    else if (o == 1) c2_sync<1>();
-    else if (o + 1 < DT || has_next_h) c2_sync<2>();
-    else c2_sync<1>();
+    else c2_sync_n(((o + 1 < DT || has_next_h) ? 1 : 0) + (o >= 3 ? S : 0));
     const u32x4* cb = pp.cur();
     if (o + 1 < DT) dma_image(pp.nxt(), Wt + (size_t)(o + 1) * TU, TU, kC2Waves, pp.wave, pp.lane);
     else if (nextW) dma_image(pp.nxt(), nextW, next_n16, kC2Waves, pp.wave, pp.lane);
     ++pp.cnt;
     if (o + 2 < DT) dma16(rh, slots + ((o + 2) & 3) * 64, voff, 64 * (o + 2));
     else if (has_next_h) dma16(rh_next, slots + ((o + 2) & 3) * 64, voff, 64 * (o + 2 - DT));
+    if (o >= 2) stores(o - 2);
     f32x4 acc;
     if (o > 0) {
       // the saved h tile of the epilogue below, read now so its LDS latency hides behind the first
@@ -237,7 +243,11 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP],
     prev = acc;
     __builtin_amdgcn_sched_barrier(0);      // no code motion across tiles (register pressure)
   }
-  epi(DT - 1, prev);
+  stores(DT - 2);
+  hc = lds_read16_issue(slots + ((DT - 1) & 3) * 64 + pp.lane);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) epi_part(DT - 1, prev, r);
+  stores(DT - 1);
 }
 
 template <int D, int KT0, int OTL, int NP>
@@ -320,17 +330,20 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) 
   }
   for (int l = nl - 2; l >= 1; --l) {
     c2_split<DT, NP>(nx, bp);
+    // first wait: after the previous layer's last weight DMA, its h DMA and the stores of its last
+    // three tiles
     c2b_layer<KB, NP>(pp, wt(l), bp, rh(l - 1), rz(l - 1), rh(l >= 2 ? l - 2 : 0), l - 1 >= 1, voff, next_img(l),
-                      c2_tile_u4(KB, NP), 3, nx);
+                      c2_tile_u4(KB, NP), 1 + 3 * (kChainGeluInPlace ? 2 : 1), nx);
   }
-  // ---- first Linear: dX = W_0^T dz_0 (KT0 output tiles); first wait: the last layer's two dz stores
+  // ---- first Linear: dX = W_0^T dz_0 (KT0 output tiles); first wait: the stores of the last layer's
+  // last three tiles
   if (a.dX) {
     c2_split<DT, NP>(nx, bp);
     const u32x4* W0 = wt(0);
     float dx[KT0][4];
 #pragma unroll
     for (int o = 0; o < KT0; ++o) {
-      if (o == 0) c2_sync<2>();
+      if (o == 0) c2_sync_n(3 * (kChainGeluInPlace ? 2 : 1));
       else c2_sync<0>();
       const u32x4* cb = pp.cur();
       if (o + 1 < KT0)

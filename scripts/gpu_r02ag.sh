@@ -1,0 +1,11 @@
+#!/bin/bash
+# chain2 backward stores delayed two tiles (dz only; and with gelu(h) in place, microbench_gh):
+# microbench, GPU suite, bench
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 200 ./gnot-replication_amd/lib/microbench 262144 256 8 > gpurun_out/ag_mb.txt 2>&1 &&
+timeout -k 10 200 ./gnot-replication_amd/lib/microbench_gh 262144 256 8 > gpurun_out/ag_mb_gh.txt 2>&1 &&
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/ag_tests.log 2>&1 &&
+timeout -k 10 400 python3 -u bench.py --breakdown > gpurun_out/ag_bench.json 2> gpurun_out/ag_bench.err
