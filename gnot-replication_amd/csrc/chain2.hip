@@ -31,6 +31,8 @@
 
 namespace gnot {
 
+constexpr int S_BWD = 1;   // vector-memory stores per backward tile (the dz tile)
+
 // LDS of one workgroup (u32x4 units): two weight-chunk buffers, two 1 KiB bias buffers (layer parity,
 // forward) and per wave four 1 KiB slots of saved pre-activation tiles (backward).
 template <int D, int NP>
@@ -193,29 +195,18 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP],
   // one part of tile o's epilogue (inside the next tile's MFMA stream): part 0 waits for the saved
   // pre-activation tile
   f32x4 hc;
-  float gh[DT][4];
   auto epi_part = [&](int o, const f32x4& acc, int r) {
     // the saved tile was read at the top of this tile (lds_read16_issue); wait for it here
     if (r == 0) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(hc) :: "memory");
-    float Phi, e;
-    gelu_parts(hc[r], Phi, e);
-    nx[o][r] = acc[r] * fmaf(hc[r] * kInvSqrt2Pi, e, Phi);
+    nx[o][r] = acc[r] * gelu_grad(hc[r]);
     asm volatile("" : "+v"(nx[o][r]));
-    if (kChainGeluInPlace) {
-      // gelu(h) = h Phi from the same erf replaces h in the save (the weight gradients' B operand,
-      // read after this kernel; nothing else reads h later)
-      gh[o][r] = hc[r] * Phi;
-      asm volatile("" : "+v"(gh[o][r]));
-    }
   };
-  // tile o's stores (dz, and gelu(h) in place) are issued at the top of tile o+2, after that tile's
-  // DMAs: a counted wait only retires the ops issued before the DMA it waits for, so each store gets
-  // two tiles to drain instead of one
+  // tile o's dz store is issued at the top of tile o+2, after that tile's DMAs: a counted wait only
+  // retires the ops issued before the DMA it waits for, so each store gets two tiles to drain
   auto stores = [&](int o) {
     buf_store_f32x4(make_float4(nx[o][0], nx[o][1], nx[o][2], nx[o][3]), rz, voff + 64 * o);
-    if (kChainGeluInPlace) buf_store_f32x4(make_float4(gh[o][0], gh[o][1], gh[o][2], gh[o][3]), rh, voff + 64 * o);
   };
-  constexpr int S = kChainGeluInPlace ? 2 : 1;          // stores per tile
+  constexpr int S = 1;                                   // stores per tile
 #pragma unroll
   for (int o = 0; o < DT; ++o) {
     // ops issued after the weight DMA this wait retires (at the top of tile o-1): that tile's h DMA
@@ -333,7 +324,7 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) 
     // first wait: after the previous layer's last weight DMA, its h DMA and the stores of its last
     // three tiles
     c2b_layer<KB, NP>(pp, wt(l), bp, rh(l - 1), rz(l - 1), rh(l >= 2 ? l - 2 : 0), l - 1 >= 1, voff, next_img(l),
-                      c2_tile_u4(KB, NP), 1 + 3 * (kChainGeluInPlace ? 2 : 1), nx);
+                      c2_tile_u4(KB, NP), 1 + 3 * S_BWD, nx);
   }
   // ---- first Linear: dX = W_0^T dz_0 (KT0 output tiles); first wait: the stores of the last layer's
   // last three tiles
@@ -343,7 +334,7 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) 
     float dx[KT0][4];
 #pragma unroll
     for (int o = 0; o < KT0; ++o) {
-      if (o == 0) c2_sync_n(3 * (kChainGeluInPlace ? 2 : 1));
+      if (o == 0) c2_sync_n(3 * S_BWD);
       else c2_sync<0>();
       const u32x4* cb = pp.cur();
       if (o + 1 < KT0)

@@ -636,8 +636,7 @@ static void build_groups(gnot_plan* p) {
     G.jobs.push_back(J);
   };
   // chain c of a group: Linear j reads dZ_j from dz[(c*NL + j)*rows*D] and its input from the
-  // chain input (j = 0) or gelu(saved pre-activation j-1) (at d = 256 with kChainGeluInPlace the
-  // chain backward has already replaced each saved h by gelu(h), so the GEMM reads it as is)
+  // chain input (j = 0) or gelu(saved pre-activation j-1)
   auto chain_group = [&](WgradGroup& G, int kcall, const std::vector<int>& firsts, long rows, const float* x0,
                          long ldx0, const float* save) {
     const float* dz = p->P_(p->dz_name(kcall));
@@ -645,8 +644,7 @@ static void build_groups(gnot_plan* p) {
       for (int j = 0; j < NL; ++j) {
         const float* dzp = dz + ((long)c * NL + j) * rows * D;
         if (j == 0) lin_job(G, firsts[c] + j, dzp, D, x0, ldx0, 0, rows);
-        else lin_job(G, firsts[c] + j, dzp, D, save + ((long)c * NL + j - 1) * rows * D, D,
-                     (D == 256 && kChainGeluInPlace) ? 0 : 1, rows);
+        else lin_job(G, firsts[c] + j, dzp, D, save + ((long)c * NL + j - 1) * rows * D, D, 1, rows);
       }
     finish_group(p, G);
   };

@@ -92,12 +92,6 @@ hipError_t launch_chain_bwd(const ChainArgs& a, hipStream_t s);
 // d = 256 chains (chain2.hip): bf16x6 in both directions, output-major x6 images (pack x6 = 2) for Wp
 // AND WpT
 hipError_t launch_chain2(const ChainArgs& a, bool bwd, hipStream_t s);
-// the d = 256 chain backward replaces each saved pre-activation h by gelu(h) in place (the weight
-// gradients then read their B operand as is, WgradJob::x_gelu = 0)
-#ifndef GNOT_GELU_INPLACE
-#define GNOT_GELU_INPLACE 0
-#endif
-constexpr bool kChainGeluInPlace = GNOT_GELU_INPLACE != 0;
 
 // ------------------------------------------------------------------ point-reduction GEMM (wgrad.hip)
 // C[out, in] = sum_p dz[p, :out]^T x[p, :in] over a point range, plus column sums of dz.
