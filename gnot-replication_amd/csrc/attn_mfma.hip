@@ -356,12 +356,19 @@ __global__ void __launch_bounds__(256) attn_kv_bwd_batch_mfma_kernel(const AttnK
 
 namespace {
 constexpr size_t kApplyLdsMax = 160 * 1024;
+// below this many 64-point chunks the MFMA passes run fewer than ~128 workgroups, each staging the
+// state images before its few chunks: the VALU kernels (attn.hip) are faster there (configs[1],
+// 10k points: apply bwd 23 vs 70 us per call; env GNOT_APPLY_MFMA_MIN overrides)
+static int mfma_min_chunks() {
+  const char* e = std::getenv("GNOT_APPLY_MFMA_MIN");    // read per launch: tests force either path
+  return e ? std::atoi(e) : 512;
+}
 
 template <int DH>
 bool mfma_ok(const AttnApplyArgs& a, bool bwd) {
   static const bool valu = std::getenv("GNOT_APPLY_VALU") != nullptr;
-  return !valu && a.nsrc >= 1 && a.nsrc <= 8 && (a.ldq & 3) == 0 && (!bwd || ((a.lddq & 3) == 0 && (a.lddu & 3) == 0)) &&
-         apply_lds_bytes<DH>(a.nsrc, a.H, bwd) <= kApplyLdsMax;
+  return !valu && a.nchunks >= mfma_min_chunks() && a.nsrc >= 1 && a.nsrc <= 8 && (a.ldq & 3) == 0 &&
+         (!bwd || ((a.lddq & 3) == 0 && (a.lddu & 3) == 0)) && apply_lds_bytes<DH>(a.nsrc, a.H, bwd) <= kApplyLdsMax;
 }
 
 template <int DH, bool BWD>
@@ -411,6 +418,7 @@ hipError_t launch_attn_kv_bwd_mfma(const AttnKVBwdArgs* a, const AttnKVBwdArgs* 
                                    int H, int dh, hipStream_t s) {
   static const bool valu = std::getenv("GNOT_APPLY_VALU") != nullptr;
   if (valu || (a && ((a->ldkv & 3) || (a->lddkv & 3)))) return hipErrorNotSupported;
+  if ((a ? a->nchunks : maxchunks * njobs) < mfma_min_chunks()) return hipErrorNotSupported;
   switch (dh) {
     case 16: if (apply_lds_bytes<16>(1, H, true) <= kApplyLdsMax) return launch_kv<16>(a, jobs_dev, njobs, maxchunks, H, s); break;
     case 32: if (apply_lds_bytes<32>(1, H, true) <= kApplyLdsMax) return launch_kv<32>(a, jobs_dev, njobs, maxchunks, H, s); break;

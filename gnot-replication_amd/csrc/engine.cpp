@@ -63,7 +63,8 @@ struct WgradGroup {
   size_t slab_floats = 0;
   bool x6 = false;                   // plain weight-gradient jobs: the bf16x6 MFMA kernel
   bool wide = false;                 // ... on the 256 x 256-tile kernel (d = 256: one workgroup per job split)
-  int state_pts = 0, state_nw = 0;   // state groups: points per workgroup, per-point weights (0 or H)
+  int state_pts = 0, state_nw = 0;
+  bool state_mfma = false;   // state groups: points per workgroup, per-point weights (0 or H)
   WgradJob* d_jobs = nullptr;        // device copies (workspace tables)
   int* d_wg_prefix = nullptr;
   int* d_red_prefix = nullptr;
@@ -565,7 +566,10 @@ static void finish_state_group(gnot_plan* p, WgradGroup& G) {
   if (!G.jobs.empty()) {
     const int d = G.jobs[0].out;
     const int dh = G.jobs[0].state_dh;
-    G.state_pts = env_pts > 0 ? (state_mfma_ok(d, dh) ? env_pts : std::min(env_pts, 8192 / d)) : state_pts(d, dh);
+    long total = 0;
+    for (const auto& J : G.jobs) total += J.P;
+    G.state_mfma = state_mfma_ok(d, dh) && total >= state_mfma_min_points();
+    G.state_pts = env_pts > 0 ? (G.state_mfma ? env_pts : std::min(env_pts, 8192 / d)) : state_pts(G.state_mfma, d);
     G.state_nw = 0;
     for (const auto& J : G.jobs)
       if (J.w != nullptr) G.state_nw = d / J.state_dh;
@@ -1413,7 +1417,7 @@ int run_state(Ctx& c, const WgradGroup& G) {
   ProfScope ps(c, "state", group_flops(G));
   GNOT_CK(launch_state(G.d_jobs, G.d_wg_prefix, (int)G.jobs.size(), G.total_wgs, G.d_red_prefix,
                        G.total_red, c.p->P_("slab_state"), G.jobs[0].out, G.jobs[0].state_dh, G.state_pts,
-                       G.state_nw, c.s));
+                       G.state_nw, G.state_mfma, c.s));
   return GNOT_OK;
 }
 

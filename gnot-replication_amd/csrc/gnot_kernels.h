@@ -132,10 +132,18 @@ inline bool state_mfma_ok(int d, int dh) {
 // points per partial-state workgroup: 256 on MFMA (4 waves per SIMD at 262k points, partials ~6 % of
 // the row bytes); VALU: the workgroup's A and B rows fill <= 32 KiB of LDS each (64 at d <= 128,
 // 8192 / d above; measured: 32 and 16 are slower at cfg2).  env GNOT_STATE_PTS overrides
-inline int state_pts(int d, int dh) { return state_mfma_ok(d, dh) ? 256 : d <= 128 ? 64 : 8192 / d; }
+inline int state_pts(bool mfma, int d) { return mfma ? 256 : d <= 128 ? 64 : 8192 / d; }
+// MFMA only from this many points in the group (env GNOT_STATE_MFMA_MIN, read per plan): below it the
+// 256-point MFMA workgroups leave most CUs idle and the 64-point VALU kernel is faster (configs[1],
+// 10k points: 3.60 vs 3.94 ms per step)
+inline long state_mfma_min_points() {
+  const char* e = std::getenv("GNOT_STATE_MFMA_MIN");
+  return e ? std::atol(e) : 65536;
+}
 hipError_t launch_state(const WgradJob* jobs_dev, const int* wg_prefix_dev, int njobs, int total_wgs,
                         const int* red_prefix_dev, int total_red, float* slab, int d, int dh, int pts, int nw,
-                        hipStream_t s);   // d: row width, pts: points per workgroup, nw: per-point weights (0 or H)
+                        bool mfma, hipStream_t s);   // d: row width, pts: points per workgroup, nw: per-point
+                                                     // weights (0 or H), mfma: state_mfma_kernel (state_mfma_ok)
 
 // ------------------------------------------------------------------ attention (attn.hip)
 struct AttnApplyArgs {

@@ -258,9 +258,10 @@ __global__ void __launch_bounds__(256) state_reduce_kernel(const WgradJob* __res
 
 hipError_t launch_state(const WgradJob* jobs_dev, const int* wg_prefix_dev, int njobs, int total_wgs,
                         const int* red_prefix_dev, int total_red, float* slab, int d, int dh, int pts, int nw,
-                        hipStream_t s) {
+                        bool mfma, hipStream_t s) {
   if (njobs <= 0 || total_wgs <= 0) return hipSuccess;
-  if (state_mfma_ok(d, dh)) {
+  if (mfma) {
+    if (!state_mfma_ok(d, dh)) return hipErrorInvalidValue;
     const int hpw = d / dh / 4;
     const dim3 grid(total_wgs), block(256);
 #define GNOT_STATE_MFMA(DHV, HPWV)                                                                             \

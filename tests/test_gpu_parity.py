@@ -30,8 +30,20 @@ def run_packed(m, fx, G):
     return out.detach().double().cpu().numpy(), grads
 
 
+@pytest.fixture(params=["auto", "mfma"])
+def attn_path(request, monkeypatch):
+    """'auto': the size-based choice (VALU attention passes below 512 point chunks and VALU state
+    reductions below 65,536 points, i.e. every fixture); 'mfma': GNOT_APPLY_MFMA_MIN=0 and
+    GNOT_STATE_MFMA_MIN=0 force the fp32-MFMA apply / K-V backward (attn_mfma.hip) and state
+    (state.hip) kernels wherever the head width has one."""
+    if request.param == "mfma":
+        monkeypatch.setenv("GNOT_APPLY_MFMA_MIN", "0")
+        monkeypatch.setenv("GNOT_STATE_MFMA_MIN", "0")
+    return request.param
+
+
 @pytest.mark.parametrize("name", fixture_names())
-def test_fixture_parity_packed(name):
+def test_fixture_parity_packed(name, attn_path):
     fx = load(name)
     m = build_model(fx["params"], fx["cfg"])
     out, grads = run_packed(m, fx, fx["G"])
@@ -126,7 +138,7 @@ def _random_case(seed, cfg, Ns, Ms):
                   n_mlp_num_layers=4, n_expert=3, n_head=8, n_input_functions=0),
          Ns=[129, 64, 1], Ms=[]),
 ])
-def test_random_config_vs_oracle(case):
+def test_random_config_vs_oracle(case, attn_path):
     fx, G = _random_case(3, case["cfg"], case["Ns"], case["Ms"])
     m = build_model(fx["params"], fx["cfg"])
     out, grads = run_packed(m, fx, G)
