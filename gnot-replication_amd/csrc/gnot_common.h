@@ -43,28 +43,32 @@ constexpr float kInvSqrt2Pi = 0.39894228040143267794f;
 
 // nn.GELU() (exact-erf form, reference model.py:10,13): gelu(x) = x * Phi(x), Phi(x) = (1 + erf(x/sqrt2))/2.
 // erf by Abramowitz-Stegun 7.1.26 (|error| <= 1.5e-7, below fp32 rounding of the result for |x| > 1):
-// one v_rcp, one v_exp and 5 FMAs instead of ocml erff's two-branch ~40-instruction sequence.  The
-// e^{-x^2/2} factor is shared with the derivative gelu'(x) = Phi(x) + x phi(x).
-GNOT_DEV void gelu_parts(float x, float& Phi, float& e) {
-  const float u = fabsf(x) * kSqrt1_2;
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, u, 1.0f));
-  float poly = fmaf(t, 1.061405429f, -1.453152027f);
-  poly = fmaf(t, poly, 1.421413741f);
-  poly = fmaf(t, poly, -0.284496736f);
-  poly = fmaf(t, poly, 0.254829592f);
-  poly *= t;
-  e = __expf(-u * u);                       // = exp(-x^2 / 2)
-  const float erf_abs = fmaf(-poly, e, 1.0f);
-  Phi = 0.5f + 0.5f * copysignf(erf_abs, x);
+// one v_rcp, one v_exp and 4 FMAs instead of ocml erff's two-branch ~40-instruction sequence.  Written
+// around the tail q = Phi(-|x|) = (1 - erf(|x|/sqrt2))/2 = t P(t) e^{-x^2/2} (the 1/2 folded into
+// P's coefficients, 1/sqrt2 into t's, log2(e)/2 into the exponent's), so that
+//   gelu(x)  = max(x, 0) - |x| q                      (no sign select: x Phi(x) = relu(x) - |x| Phi(-|x|))
+//   gelu'(x) = Phi(x) + x phi(x),  Phi(x) = 1/2 + sign(x) (1/2 - q),  phi(x) = e^{-x^2/2} / sqrt(2 pi)
+// 13 VALU for gelu (the chain epilogues run beside MFMAs, where VALU issue is the scarce resource).
+GNOT_DEV float gelu_tail(float x, float& e) {
+  const float t = __builtin_amdgcn_rcpf(fmaf(fabsf(x), 0.3275911f * kSqrt1_2, 1.0f));
+  float P = fmaf(t, 0.5f * 1.061405429f, 0.5f * -1.453152027f);
+  P = fmaf(t, P, 0.5f * 1.421413741f);
+  P = fmaf(t, P, 0.5f * -0.284496736f);
+  P = fmaf(t, P, 0.5f * 0.254829592f);
+  e = __builtin_amdgcn_exp2f(x * (x * -0.72134752044448170368f));   // 2^(-x^2 log2(e) / 2) = e^{-x^2/2}
+  return (P * t) * e;
 }
 GNOT_DEV float gelu(float x) {
-  float Phi, e;
-  gelu_parts(x, Phi, e);
-  return x * Phi;
+  float e;
+  const float q = gelu_tail(x, e);
+  float r;                                  // max(x, 0) without fmaxf's NaN-quieting v_max(x, x)
+  asm("v_max_f32 %0, 0, %1" : "=v"(r) : "v"(x));
+  return fmaf(-fabsf(x), q, r);
 }
 GNOT_DEV float gelu_grad(float x) {
-  float Phi, e;
-  gelu_parts(x, Phi, e);
+  float e;
+  const float q = gelu_tail(x, e);
+  const float Phi = 0.5f + copysignf(0.5f - q, x);
   return fmaf(x * kInvSqrt2Pi, e, Phi);
 }
 
@@ -301,6 +305,8 @@ template <int D>
 constexpr int x6_chunk_f4(int KT, int OT) { return x6_och<D>(KT, OT) * x6_tch<D>(KT, OT) * 3 * WAVE; }
 
 GNOT_DEV unsigned f2u(float x) { return __builtin_bit_cast(unsigned, x); }
+// (hi & 0xFFFF0000) | (lo >> 16) in one v_perm_b32: the high halves of two words as two bf16
+GNOT_DEV unsigned pack_hi16(unsigned hi, unsigned lo) { return __builtin_amdgcn_perm(hi, lo, 0x07060302u); }
 GNOT_DEV float u2f(unsigned x) { return __builtin_bit_cast(float, x); }
 
 // ---- buffer loads: base + bound in SGPRs (reads past `bytes` return 0), wave-uniform row offset in
@@ -345,9 +351,9 @@ GNOT_DEV void split8_x6(const float (&v)[8], u32x4 (&p)[3]) {
   }
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
-    p[0][d] = (w0[2 * d + 1] & 0xFFFF0000u) | (w0[2 * d] >> 16);
-    p[1][d] = (w1[2 * d + 1] & 0xFFFF0000u) | (w1[2 * d] >> 16);
-    p[2][d] = (w2[2 * d + 1] & 0xFFFF0000u) | (w2[2 * d] >> 16);
+    p[0][d] = pack_hi16(w0[2 * d + 1], w0[2 * d]);
+    p[1][d] = pack_hi16(w1[2 * d + 1], w1[2 * d]);
+    p[2][d] = pack_hi16(w2[2 * d + 1], w2[2 * d]);
   }
 }
 
@@ -377,9 +383,9 @@ GNOT_DEV void split2_np(float v0, float v1, u32x4 (&p)[NP], int d) {
     const float ra = v0 - u2f(a0 & 0xFFFF0000u), rb = v1 - u2f(b0 & 0xFFFF0000u);
     const unsigned a1 = f2u(ra), b1 = f2u(rb);
     const unsigned a2 = f2u(ra - u2f(a1 & 0xFFFF0000u)), b2 = f2u(rb - u2f(b1 & 0xFFFF0000u));
-    p[0][d] = (b0 & 0xFFFF0000u) | (a0 >> 16);
-    p[1][d] = (b1 & 0xFFFF0000u) | (a1 >> 16);
-    p[2][d] = (b2 & 0xFFFF0000u) | (a2 >> 16);
+    p[0][d] = pack_hi16(b0, a0);
+    p[1][d] = pack_hi16(b1, a1);
+    p[2][d] = pack_hi16(b2, a2);
   } else {
     p[0][d] = (bf16_rne_bits(v1) << 16) | bf16_rne_bits(v0);
   }

@@ -521,7 +521,8 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
       // point the split of the pair just finished), then that point's row loads for stage pn.
       // sched_barrier pins the order, so each wave alternates MFMA groups and VALU chunks and the two
       // waves of a SIMD fill each other's gaps.
-      auto fused = [&](int b, long pn, auto GEL) {
+      // MASK: columns past out / in exist (the fa / fb selects); jobs with out = in = 256 skip them
+      auto fused = [&](int b, long pn, auto GEL, auto MASK) {
         const u32x4* A = wl + b * w_buf(NP);
         const u32x4* Bm = A + NP * kWPiece;
         u32x4 bf[2][NP], af[2][NP], pa[NP], pq[NP];
@@ -534,12 +535,10 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
         float ra[8], vb[8];
         const unsigned pr = (unsigned)(pn + 8 * hw);
         auto chunk = [&](int k) {
-          ra[k] = fa ? R.a[k] : 0.f;
+          ra[k] = (!decltype(MASK)::value || fa) ? R.a[k] : 0.f;
           dbacc += ra[k];
-          const float bv = fb ? R.b[k] : 0.f;
+          const float bv = (!decltype(MASK)::value || fb) ? R.b[k] : 0.f;
           vb[k] = decltype(GEL)::value ? gelu(bv) : bv;
-          R.a[k] = buf_load_f32(rA, voA, (int)((pr + k) * (unsigned)J.lddz * 4u));
-          R.b[k] = buf_load_f32(rB, voB, (int)((pr + k) * (unsigned)J.ldx * 4u));
           // pin the chunk's results here: IR-level sinking would otherwise move the whole staging
           // next to its LDS stores after the last MFMA group (sched_barrier only binds the scheduler)
           asm volatile("" : "+v"(ra[k]), "+v"(vb[k]), "+v"(dbacc));
@@ -548,6 +547,13 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
             split2_np<NP>(vb[k - 1], vb[k], pq, k >> 1);
 #pragma unroll
             for (int q = 0; q < NP; ++q) asm volatile("" : "+v"(pa[q][k >> 1]), "+v"(pq[q][k >> 1]));
+            // the pair's row loads for stage pn only after its split: the raw registers are then dead
+            // and are reloaded in place (loading them earlier forces a copy of every raw value)
+#pragma unroll
+            for (int kk = k - 1; kk <= k; ++kk) {
+              R.a[kk] = buf_load_f32(rA, voA, (int)((pr + kk) * (unsigned)J.lddz * 4u));
+              R.b[kk] = buf_load_f32(rB, voB, (int)((pr + kk) * (unsigned)J.ldx * 4u));
+            }
           }
         };
 #pragma unroll
@@ -572,16 +578,21 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
           base[(NP + q) * kWPiece + sdst] = pq[q];
         }
       };
-      auto run = [&](auto GEL) {
+      auto run = [&](auto GEL, auto MASK) {
         for (; p0 + kWStage < pe; p0 += kWStage) {
-          fused(buf, p0 + 2 * kWStage, GEL);
+          fused(buf, p0 + 2 * kWStage, GEL, MASK);
           __syncthreads();
           buf ^= 1;
         }
       };
       if (full) {
-        if (gel) run(std::true_type{});
-        else run(std::false_type{});
+        if (J.out >= 256 && J.in >= 256) {
+          if (gel) run(std::true_type{}, std::false_type{});
+          else run(std::false_type{}, std::false_type{});
+        } else {
+          if (gel) run(std::true_type{}, std::true_type{});
+          else run(std::false_type{}, std::true_type{});
+        }
       } else {
         for (; p0 + kWStage < pe; p0 += kWStage) {
           compute(buf);
