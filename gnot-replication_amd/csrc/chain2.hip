@@ -25,6 +25,9 @@
 #ifndef GNOT_C2_AHEAD_F
 #define GNOT_C2_AHEAD_F true
 #endif
+#ifndef GNOT_C2F_DMA_UNROLL
+#define GNOT_C2F_DMA_UNROLL 1
+#endif
 #ifndef GNOT_C2_AHEAD_B
 #define GNOT_C2_AHEAD_B true
 #endif
@@ -75,23 +78,31 @@ GNOT_DEV void c2f_layer(C2Pipe& pp, const u32x4* W, const u32x4 (&in)[KBI][NP], 
     if (o == 0) c2_sync_n(pend0);
     else c2_sync_n((SAVE && o >= 2) ? 1 : 0);
     const u32x4* cb = pp.cur();
-    if (o + 1 < OT) {
-      dma_image(pp.nxt(), W + (size_t)(o + 1) * TU, TU, kC2Waves, pp.wave, pp.lane);
-    } else if (nextW) {
-      // the next layer's bias first: the next layer's first wait only counts ops after its weights
-      if (pp.wave == 0)
-        dma16(make_rsrc(next_bias, (unsigned)next_bias_bytes), pp.lds + C2Lds<256, NP>::kBias + (bsel ^ 1) * 64,
-              pp.lane * 16, 0);
-      dma_image(pp.nxt(), nextW, next_n16, kC2Waves, pp.wave, pp.lane);
-    }
+    u32x4* nb = pp.nxt();
     ++pp.cnt;
+    auto issue = [&]() __attribute__((always_inline)) {
+      if (o + 1 < OT) {
+#if GNOT_C2F_DMA_UNROLL
+        dma_image_n<TU, kC2Waves>(nb, W + (size_t)(o + 1) * TU, pp.wave, pp.lane);
+#else
+        dma_image(nb, W + (size_t)(o + 1) * TU, TU, kC2Waves, pp.wave, pp.lane);
+#endif
+      } else if (nextW) {
+        // the next layer's bias first: the next layer's first wait only counts ops after its weights
+        if (pp.wave == 0)
+          dma16(make_rsrc(next_bias, (unsigned)next_bias_bytes), pp.lds + C2Lds<256, NP>::kBias + (bsel ^ 1) * 64,
+                pp.lane * 16, 0);
+        dma_image(nb, nextW, next_n16, kC2Waves, pp.wave, pp.lane);
+      }
+    };
     const u32x4 bb = bias[4 * o + g];
     f32x4 acc;
     if (o > 0) {
       const f32x4 pv = prev;
       auto ep = [&](int r) { epi_part(o - 1, pv, r); };
-      acc = c2_tile_epi<KBI, NP, GNOT_C2_AHEAD_F>(cb, in, __builtin_bit_cast(f32x4, bb), pp.lane, ep);
+      acc = c2_tile_epi<KBI, NP, GNOT_C2_AHEAD_F>(cb, in, __builtin_bit_cast(f32x4, bb), pp.lane, ep, issue);
     } else {
+      issue();
       acc = c2_tile<KBI, false, NP>(cb, in, __builtin_bit_cast(f32x4, bb), pp.lane);
     }
     prev = acc;
@@ -214,9 +225,12 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP],
     if (o == 0) c2_sync_n(pend0);
     else c2_sync_n(((o + 1 < DT || has_next_h) ? 1 : 0) + (o >= 3 ? S : 0));
     const u32x4* cb = pp.cur();
-    if (o + 1 < DT) dma_image(pp.nxt(), Wt + (size_t)(o + 1) * TU, TU, kC2Waves, pp.wave, pp.lane);
-    else if (nextW) dma_image(pp.nxt(), nextW, next_n16, kC2Waves, pp.wave, pp.lane);
+    u32x4* nb = pp.nxt();
     ++pp.cnt;
+    // (unlike the forward, the DMA issue stays ahead of k-block 0's fragment reads here, and in its
+    // loop form: after the reads 153 -> 144 TFLOP/s, unrolled 149 -> 141)
+    if (o + 1 < DT) dma_image(nb, Wt + (size_t)(o + 1) * TU, TU, kC2Waves, pp.wave, pp.lane);
+    else if (nextW) dma_image(nb, nextW, next_n16, kC2Waves, pp.wave, pp.lane);
     if (o + 2 < DT) dma16(rh, slots + ((o + 2) & 3) * 64, voff, 64 * (o + 2));
     else if (has_next_h) dma16(rh_next, slots + ((o + 2) & 3) * 64, voff, 64 * (o + 2 - DT));
     if (o >= 2) stores(o - 2);

@@ -55,13 +55,22 @@ GNOT_DEV f32x4 c2_tile(const u32x4* __restrict__ cb, const u32x4 (&bp)[KB][NP], 
 // the epilogue pins its results with empty asm (IR sinking would otherwise move them to their uses), so
 // the VALU issues in this wave's own MFMA shadows instead of as one burst after the tile that both
 // waves of a SIMD reach together.
-template <int KB, int NP, bool AHEAD, typename Epi>
-GNOT_DEV f32x4 c2_tile_epi(const u32x4* __restrict__ cb, const u32x4 (&bp)[KB][NP], f32x4 acc, int lane, Epi&& epi) {
+// `pre` runs right after k-block 0's fragment reads are issued (the tile's DMA issue goes there, so its
+// issue time overlaps their LDS latency instead of delaying them behind the barrier).
+struct C2NoPre {
+  GNOT_DEV void operator()() const {}
+};
+template <int KB, int NP, bool AHEAD, typename Epi, typename Pre = C2NoPre>
+GNOT_DEV f32x4 c2_tile_epi(const u32x4* __restrict__ cb, const u32x4 (&bp)[KB][NP], f32x4 acc, int lane, Epi&& epi,
+                           Pre&& pre = Pre()) {
   u32x4 ab[AHEAD ? 2 : 1][NP];
   if (AHEAD) {
 #pragma unroll
     for (int q = 0; q < NP; ++q) ab[0][q] = cb[q * WAVE + lane];
   }
+  __builtin_amdgcn_sched_barrier(0);
+  pre();
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int t = 0; t < KB; ++t) {
     if (AHEAD) {
@@ -190,6 +199,18 @@ GNOT_DEV void dma_image(u32x4* lds, const void* src, int n16, int nwaves, int wa
   // every DMA into a waterfall loop
   const int w = __builtin_amdgcn_readfirstlane(wave);
   for (int base = w * WAVE; base < n16; base += nwaves * WAVE) dma16(r, lds + base, lane * 16, base * 16);
+}
+
+// the same with the size known at compile time: unrolled (no loop counter and branch per DMA)
+template <int N16, int NW>
+GNOT_DEV void dma_image_n(u32x4* lds, const void* src, int wave, int lane) {
+  const rsrc_t r = make_rsrc(src, (unsigned)N16 * 16u);
+  const int w = __builtin_amdgcn_readfirstlane(wave);
+#pragma unroll
+  for (int i = 0; i < (N16 + NW * WAVE - 1) / (NW * WAVE); ++i) {
+    const int base = (w + i * NW) * WAVE;
+    if ((i + 1) * NW * WAVE <= N16 || base < N16) dma16(r, lds + base, lane * 16, base * 16);
+  }
 }
 
 template <int KT, int NP = 3>
