@@ -388,6 +388,14 @@ GNOT_DEV void mfma_np(const u32x4 (&a)[NP], const u32x4 (&b)[NP], f32x16& c) {
   else c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[0]), __builtin_bit_cast(bf16x8, b[0]), c, 0, 0, 0);
 }
 
+// the wide kernel's row loads; GNOT_WGRAD_AUX: their cache-policy bits (0 default, 2 nt)
+#ifndef GNOT_WGRAD_AUX
+#define GNOT_WGRAD_AUX 0
+#endif
+GNOT_DEV float wrow_load(rsrc_t r, int voff, int soff) {
+  return u2f(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, GNOT_WGRAD_AUX));
+}
+
 template <int V, int NP = 3>
 __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __restrict__ jobs,
                                                               const int* __restrict__ prefix, int njobs,
@@ -433,8 +441,8 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
     // raw values only: any arithmetic on them here would make the wave wait for the load now
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      R.a[k] = buf_load_f32(rA, voA, (int)((pr + k) * (unsigned)J.lddz * 4u));
-      R.b[k] = buf_load_f32(rB, voB, (int)((pr + k) * (unsigned)J.ldx * 4u));
+      R.a[k] = wrow_load(rA, voA, (int)((pr + k) * (unsigned)J.lddz * 4u));
+      R.b[k] = wrow_load(rB, voB, (int)((pr + k) * (unsigned)J.ldx * 4u));
     }
   };
   // split + LDS store of the staged rows; gel is uniform per workgroup: one branch around the whole
@@ -551,8 +559,8 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
             // and are reloaded in place (loading them earlier forces a copy of every raw value)
 #pragma unroll
             for (int kk = k - 1; kk <= k; ++kk) {
-              R.a[kk] = buf_load_f32(rA, voA, (int)((pr + kk) * (unsigned)J.lddz * 4u));
-              R.b[kk] = buf_load_f32(rB, voB, (int)((pr + kk) * (unsigned)J.ldx * 4u));
+              R.a[kk] = wrow_load(rA, voA, (int)((pr + kk) * (unsigned)J.lddz * 4u));
+              R.b[kk] = wrow_load(rB, voB, (int)((pr + kk) * (unsigned)J.ldx * 4u));
             }
           }
         };
