@@ -28,6 +28,9 @@
 #ifndef GNOT_C2F_DMA_UNROLL
 #define GNOT_C2F_DMA_UNROLL 1
 #endif
+#ifndef GNOT_C2F_PAIR
+#define GNOT_C2F_PAIR 1        // forward pair mode (two output tiles per chunk): 0 never, 1 bf16 mode, 2 always
+#endif
 #ifndef GNOT_C2B_PRE
 #define GNOT_C2B_PRE 0
 #endif
@@ -41,9 +44,15 @@ constexpr int S_BWD = 1;   // vector-memory stores per backward tile (the dz til
 
 // LDS of one workgroup (u32x4 units): two weight-chunk buffers, two 1 KiB bias buffers (layer parity,
 // forward) and per wave four 1 KiB slots of saved pre-activation tiles (backward).
+// forward pair mode: two output tiles per weight chunk, one barrier per pair.  Measured (`r02bf`):
+// bf16 mode chain forward 348 -> 388 TFLOP/s; bf16x6 unchanged (202), so only the one-piece mode
+template <int NP>
+constexpr bool c2f_pair() { return GNOT_C2F_PAIR == 2 || (GNOT_C2F_PAIR == 1 && NP == 1); }
+
 template <int D, int NP>
 struct C2Lds {
-  static constexpr int WB = c2_tile_u4(D / 32, NP);     // one output tile of a D x D image
+  // one weight chunk: one output tile of a D x D image (two in the forward's pair mode)
+  static constexpr int WB = c2_tile_u4(D / 32, NP) * (c2f_pair<NP>() ? 2 : 1);
   static constexpr int kBias = 2 * WB;                  // offset of the bias buffers
   static constexpr int kHs = kBias + 2 * 64;            // offset of the saved-row slots
   static constexpr int kBytes = (kHs + kC2Waves * 4 * 64) * 16;
@@ -76,6 +85,51 @@ GNOT_DEV void c2f_layer(C2Pipe& pp, const u32x4* W, const u32x4 (&in)[KBI][NP], 
     out[o][r] = GELU ? gelu(acc[r]) : acc[r];
     asm volatile("" : "+v"(out[o][r]));
   };
+  if constexpr (c2f_pair<NP>()) {
+  // pair mode: one chunk = tiles o, o+1; the wait at pair o retires the DMA issued at pair o-2, after
+  // which this wave issued the save stores of the epilogues inside tiles o-2 (if o-2 > 0) and o-1
+#pragma unroll
+  for (int o = 0; o < OT; o += 2) {
+    if (o == 0) c2_sync_n(pend0);
+    else c2_sync_n(SAVE ? (o >= 4 ? 2 : 1) : 0);
+    const u32x4* cb = pp.cur();
+    u32x4* nb = pp.nxt();
+    ++pp.cnt;
+    auto issue = [&]() __attribute__((always_inline)) {
+      if (o + 3 < OT) {
+        dma_image_n<2 * TU, kC2Waves>(nb, W + (size_t)(o + 2) * TU, pp.wave, pp.lane);
+      } else if (o + 2 < OT) {
+        dma_image_n<TU, kC2Waves>(nb, W + (size_t)(o + 2) * TU, pp.wave, pp.lane);
+      } else if (nextW) {
+        if (pp.wave == 0)
+          dma16(make_rsrc(next_bias, (unsigned)next_bias_bytes), pp.lds + C2Lds<256, NP>::kBias + (bsel ^ 1) * 64,
+                pp.lane * 16, 0);
+        dma_image(nb, nextW, next_n16, kC2Waves, pp.wave, pp.lane);
+      }
+    };
+    {
+      const u32x4 bb = bias[4 * o + g];
+      f32x4 acc;
+      if (o > 0) {
+        const f32x4 pv = prev;
+        auto ep = [&](int r) { epi_part(o - 1, pv, r); };
+        acc = c2_tile_epi<KBI, NP, GNOT_C2_AHEAD_F>(cb, in, __builtin_bit_cast(f32x4, bb), pp.lane, ep, issue);
+      } else {
+        issue();
+        acc = c2_tile<KBI, false, NP>(cb, in, __builtin_bit_cast(f32x4, bb), pp.lane);
+      }
+      prev = acc;
+    }
+    if (o + 1 < OT) {
+      const u32x4 bb = bias[4 * (o + 1) + g];
+      const f32x4 pv = prev;
+      auto ep = [&](int r) { epi_part(o, pv, r); };
+      prev = c2_tile_epi<KBI, NP, GNOT_C2_AHEAD_F>(cb + TU, in, __builtin_bit_cast(f32x4, bb), pp.lane, ep);
+    }
+  }
+  epi(OT - 1, prev);
+  return;
+  }
 #pragma unroll
   for (int o = 0; o < OT; ++o) {
     if (o == 0) c2_sync_n(pend0);
@@ -129,10 +183,13 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) 
   C2Pipe pp{c2lds, LD::WB, 0, wave, lane};
   const u32x4* W0 = reinterpret_cast<const u32x4*>(L[0].Wp);
   if (wave == 0) dma16(make_rsrc(L[0].bias, 16 * DT * 4), c2lds + LD::kBias, lane * 16, 0);
-  dma_image(c2lds, W0, c2_tile_u4(KB0, NP), kC2Waves, wave, lane);
+  constexpr int CH = c2f_pair<NP>() ? 2 : 1;         // output tiles per weight chunk
+  dma_image(c2lds, W0, CH * c2_tile_u4(KB0, NP), kC2Waves, wave, lane);
   auto wp = [&](int l) { return reinterpret_cast<const u32x4*>(L[l].Wp); };
   auto rs = [&](int l) { return make_rsrc(SAVE ? save + l * a.save_layer_stride : nullptr, SAVE ? lay_bytes : 0u); };
-  constexpr int pend_next = SAVE ? 2 : 0;    // a layer's first wait: the previous layer's last two saves
+  // a layer's first wait: the saves the previous layer issued after its last weight DMA (its last
+  // tile's stream + the final epilogue; pair mode: its last pair's two tiles + the final epilogue)
+  constexpr int pend_next = SAVE ? (CH == 2 ? 3 : 2) : 0;
 
   float nx[DT][4];                                   // next layer input (fp32), then split
   u32x4 bp[KB][NP];
@@ -143,15 +200,17 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) 
     u32x4 b0[KB0][NP];
     c2_split<KT0, NP>(x0, b0);
     const int nb = nl - 1 == 1 ? 16 * OTL * 4 : 16 * DT * 4;
-    c2f_layer<DT, KB0, true, SAVE, NP>(pp, W0, b0, bsel, rs(0), voff, wp(1), c2_tile_u4(KB, NP), L[1].bias, nb, 0, g,
-                                       nx);
+    c2f_layer<DT, KB0, true, SAVE, NP>(pp, W0, b0, bsel, rs(0), voff, wp(1),
+                                       (nl - 1 == 1 ? (OTL < CH ? OTL : CH) : CH) * c2_tile_u4(KB, NP), L[1].bias, nb, 0,
+                                       g, nx);
     bsel ^= 1;
   }
   for (int l = 1; l < nl - 1; ++l) {
     c2_split<DT, NP>(nx, bp);
     const int nb = l + 1 == nl - 1 ? 16 * OTL * 4 : 16 * DT * 4;
-    c2f_layer<DT, KB, true, SAVE, NP>(pp, wp(l), bp, bsel, rs(l), voff, wp(l + 1), c2_tile_u4(KB, NP), L[l + 1].bias,
-                                      nb, pend_next, g, nx);
+    c2f_layer<DT, KB, true, SAVE, NP>(pp, wp(l), bp, bsel, rs(l), voff, wp(l + 1),
+                                      (l + 1 == nl - 1 ? (OTL < CH ? OTL : CH) : CH) * c2_tile_u4(KB, NP),
+                                      L[l + 1].bias, nb, pend_next, g, nx);
     bsel ^= 1;
   }
   float y[OTL][4];
