@@ -672,7 +672,10 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
       }
   if (J.db != nullptr) {
     // column sums of A: the two point halves of every feature through LDS, in a fixed order
+    // (red overlays stage buffer 0, which other waves may still be reading in the last compute(): the
+    // V & 4 loop ends without a barrier)
     float* red = reinterpret_cast<float*>(wl);
+    __syncthreads();
     red[hh * 256 + f] = dbacc;
     __syncthreads();
     if (tid < 256 && f < J.out)
