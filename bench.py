@@ -45,15 +45,21 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: "Peak BF16/FP16 MFMA ~2.5
 HBM_PEAK_GBS = 8000.0
 
 
-def pmc_traffic(workload, kind):
-    """HBM bytes per launch of the roofline kernel, from the rocprofv3 PMC passes of the same bench
-    command (profiles/pmc_traffic.json, written by scripts/pmc_traffic.py: FETCH_SIZE x 2 for the gfx950
-    half-count of wide streaming reads + WRITE_SIZE, MI355X_MICROARCH.md HBM section), or None."""
+def pmc_traffic(workload, kind, launches_per_step):
+    """Mean HBM bytes per launch of the roofline class, from rocprofv3 PMC passes of the same bench command
+    (profiles/pmc_traffic.json, written by scripts/pmc_traffic.py: FETCH_SIZE x 2 for the gfx950 half-count
+    of wide streaming reads + WRITE_SIZE, MI355X_MICROARCH.md HBM section, summed over ALL of the class's
+    dispatches of a step and divided by their count -- the same per-launch mean as `achieved`).  None
+    when no entry exists or the entry's launches per step differ from this run's (another tree)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
-        return json.load(open(path))[f"{workload}/{kind}"]["bytes_per_launch"]
+        e = json.load(open(path))[f"{workload}/{kind}"]
     except (OSError, KeyError, ValueError):
         return None
+    if e.get("launches_per_step") != launches_per_step:
+        return None
+    return e["bytes_per_launch"]
+
 
 WORKLOADS = {
     # BASELINE.json configs[1]
@@ -187,13 +193,42 @@ def make_batch(w, seed, device):
 CPU_SAMPLE_POINTS = 16384      # bound on the CPU sample (points per step; ~10-30 s of host work)
 
 
-def cpu_baseline(w, steps=3, warmup=1):
+def host_cores():
+    """(threads to use, description): the physical cores among the CPUs this process may run on
+    (sched_getaffinity + sysfs topology: one thread per core, no SMT siblings), capped by the cgroup CPU
+    quota (a GPU box grants a share of a larger machine), as BASELINE.md's CPU plan asks."""
+    cpus = sorted(os.sched_getaffinity(0))
+    cores = set()
+    for c in cpus:
+        try:
+            base = f"/sys/devices/system/cpu/cpu{c}/topology/"
+            cores.add((open(base + "physical_package_id").read().strip(), open(base + "core_id").read().strip()))
+        except OSError:
+            cores.add(("?", str(c)))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    n = len(cores) if quota is None else min(len(cores), quota)
+    desc = (f"{n} threads = physical cores available to the process ({len(cpus)} CPUs in the affinity mask, "
+            f"{len(cores)} physical cores" + (f", cgroup CPU quota {quota}" if quota is not None else "") + ")")
+    return n, desc
+
+
+def cpu_baseline(w, steps=5, warmup=2):
     """Reference CPU path (stock torch, oracle/torch_port.py) on this host's cores, on a BOUNDED sample
     of the workload: the same model, one step over at most CPU_SAMPLE_POINTS query points (pts/s of
-    this linear-attention model is flat in the mesh size)."""
+    this linear-attention model is flat in the mesh size).  BASELINE.md's plan:
+    torch.set_num_threads(physical cores), 2 warm-up steps, median of 5."""
     from oracle import torch_port
     from gnot_amd import GNOT
     m = w["model"]
+    nthreads, cores_desc = host_cores()
+    prev_threads = torch.get_num_threads()
+    torch.set_num_threads(nthreads)
     torch.manual_seed(0)
     mod = GNOT(*[m[k] for k in ("input_dim", "theta_dim", "input_func_dim", "out_dim", "n_attn_layers",
                                 "n_attn_hidden_dim", "n_mlp_num_layers", "n_mlp_hidden_dim",
@@ -219,11 +254,12 @@ def cpu_baseline(w, steps=3, warmup=1):
         if it >= warmup:
             times.append(time.perf_counter() - t0)
     med = statistics.median(times)
-    return dict(value=round(B * N / med, 1), unit="points/s", cores=torch.get_num_threads(), kind="port",
+    torch.set_num_threads(prev_threads)
+    return dict(value=round(B * N / med, 1), unit="points/s", cores=nthreads, kind="port",
                 sample=f"bounded sample of the workload: same model, {B} mesh(es) x {N} points ({M} input-function "
                        f"points), stock-torch fp32 CPU port of the reference (oracle/torch_port.py, fixture-"
-                       f"validated), fwd+RelL2+bwd, median of {steps} steps after {warmup} warm-up, "
-                       f"{torch.get_num_threads()} threads; points/s is flat in the mesh size (linear attention)")
+                       f"validated), fwd+RelL2+bwd, median of {steps} steps after {warmup} warm-up; {cores_desc}; "
+                       f"points/s is flat in the mesh size (linear attention)")
 
 
 def main():
@@ -372,20 +408,33 @@ def main():
         opt_step()
 
     def roofline(M, dtype):
-        """the device-time-dominant kernel class of a measure() run against the dense MFMA peak of the
-        arithmetic it runs (fp32: the fp32 MFMA rate -- bf16x6 computes fp32; bf16: the bf16 rate)"""
+        """the device-time-dominant kernel class of a measure() run.  `frac` is against the dense MFMA peak of
+        the path's arithmetic type (fp32 runs: the fp32 MFMA rate; bf16 mode: the bf16 rate).  `frac_pipe` is
+        against the pipe the kernel actually issues on: the bf16x6 kernels run six bf16 MFMAs per fp32 block
+        product, so their hardware ceiling is 2.5 PFLOP/s / 6 of fp32-equivalent work (bf16 mode: / 1)."""
         avg_ms = M["kms"] / max(M["klaunch"], 1)
-        ach = (M["kflops"] / max(M["klaunch"], 1)) / (avg_ms * 1e-3) / 1e12 if M["klaunch"] and M["kms"] > 0 else 0.0
+        flops_launch = M["kflops"] / max(M["klaunch"], 1)
+        ach = flops_launch / (avg_ms * 1e-3) / 1e12 if M["klaunch"] and M["kms"] > 0 else 0.0
         peak = FP32_MFMA_PEAK_TFLOPS if dtype == "fp32" else BF16_MFMA_PEAK_TFLOPS
         form = "bf16x6" if dtype == "fp32" else "bf16"
+        d256 = m["n_attn_hidden_dim"] == 256
         names = ({"moe_fwd": f"chain2_fwd_kernel (fused MoE expert chains, forward, {form} MFMA)",
                   "moe_bwd": f"chain2_bwd_kernel (fused MoE expert chains, backward, {form} MFMA)",
                   "wgrad": f"pgemm_x6w_kernel+pgemm_reduce_kernel (weight gradients, 256x256 {form} MFMA)"}
-                 if m["n_attn_hidden_dim"] == 256 else
-                 {"moe_fwd": "chain_fwd_kernel (fused MoE expert chains, forward)",
-                  "moe_bwd": "chain_bwd_kernel (fused MoE expert chains, backward)",
+                 if d256 else
+                 {"moe_fwd": "chain_fwd_kernel (fused MoE expert chains, forward, bf16x6 MFMA)",
+                  "moe_bwd": "chain_bwd_kernel (fused MoE expert chains, backward, fp32 MFMA)",
                   "wgrad": "pgemm_x6_kernel+pgemm_reduce_kernel (weight gradients, bf16x6 MFMA)"})
         rk = M["rkind"]
+        if dtype == "bf16" and d256:
+            pipe, pipe_peak = "bf16 MFMA (one product per block)", BF16_MFMA_PEAK_TFLOPS
+        elif not d256 and rk == "moe_bwd":
+            pipe, pipe_peak = "fp32 MFMA", FP32_MFMA_PEAK_TFLOPS
+        else:
+            pipe, pipe_peak = "bf16 MFMA, six per fp32 block product (bf16x6)", BF16_MFMA_PEAK_TFLOPS / 6
+        traffic = None
+        if not args.points and dtype == "fp32":
+            traffic = pmc_traffic(args.workload, rk, M["klaunch_step"])
         return {
             "kernel": names[rk],
             "class": rk,
@@ -395,9 +444,12 @@ def main():
             "peak": peak,
             "unit": "TFLOP/s",
             "frac": round(ach / peak, 4),
-            "traffic": None if (args.points or dtype != "fp32") else pmc_traffic(args.workload, rk),
+            "pipe": pipe,
+            "pipe_peak": round(pipe_peak, 2),
+            "frac_pipe": round(ach / pipe_peak, 4),
+            "traffic": traffic,
             "avg_launch_us": round(avg_ms * 1e3, 2),
-            "flops_per_launch": M["kflops"] / max(M["klaunch"], 1),
+            "flops_per_launch": flops_launch,
             "launches": M["klaunch"],
         }
 
@@ -477,7 +529,8 @@ def main():
             t = torch.tensor([elapsed], device=device, dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
-        return dict(elapsed=elapsed, kinds=kinds, rkind=rkind, kms=kms, klaunch=klaunch, kflops=kflops)
+        return dict(elapsed=elapsed, kinds=kinds, rkind=rkind, kms=kms, klaunch=klaunch, kflops=kflops,
+                    klaunch_step=kinds[rkind][1])
 
     M0 = measure()
     elapsed, kinds, rkind, kms, klaunch, kflops = (M0[k] for k in ("elapsed", "kinds", "rkind", "kms", "klaunch", "kflops"))

@@ -179,7 +179,9 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) 
   const ChainLayer* L = a.layers + e * nl;
   float* save = SAVE ? a.save + e * a.save_chain_stride : nullptr;
   const unsigned lay_bytes = (unsigned)min((long)a.P * D * 4, 0xFFFFFFFFL);   // one [P, D] layer
-  const int voff = (int)((blockIdx.x * kC2Waves + wave) * 16 + (lane & 15)) * D * 4 + 16 * g;
+  // byte offset of this lane's row in a [P, D] layer: unsigned (the plan bounds P * D * 4 < 2^32)
+  const int voff = (int)(((unsigned)(blockIdx.x * kC2Waves + wave) * 16u + (unsigned)(lane & 15)) * (unsigned)(D * 4) +
+                         16u * (unsigned)g);
   C2Pipe pp{c2lds, LD::WB, 0, wave, lane};
   const u32x4* W0 = reinterpret_cast<const u32x4*>(L[0].Wp);
   if (wave == 0) dma16(make_rsrc(L[0].bias, 16 * DT * 4), c2lds + LD::kBias, lane * 16, 0);
@@ -337,7 +339,9 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) 
   const float* save = a.save + e * a.save_chain_stride;
   float* dz = a.dz + e * a.dz_chain_stride;
   const unsigned lay_bytes = (unsigned)min((long)a.P * D * 4, 0xFFFFFFFFL);   // one [P, D] layer
-  const int voff = (int)((blockIdx.x * kC2Waves + wave) * 16 + (lane & 15)) * D * 4 + 16 * g;
+  // byte offset of this lane's row in a [P, D] layer: unsigned (the plan bounds P * D * 4 < 2^32)
+  const int voff = (int)(((unsigned)(blockIdx.x * kC2Waves + wave) * 16u + (unsigned)(lane & 15)) * (unsigned)(D * 4) +
+                         16u * (unsigned)g);
   C2Pipe pp{c2lds, LD::WB, 0, wave, lane};
   auto wt = [&](int l) { return reinterpret_cast<const u32x4*>(L[l].WpT); };
   auto rh = [&](int l) { return make_rsrc(save + l * a.save_layer_stride, lay_bytes); };   // h_l

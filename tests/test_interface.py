@@ -110,6 +110,29 @@ def test_plan_rejects_bad_config_and_batch():
         lib.gnot_plan_destroy(plan)
 
 
+def test_plan_rejects_meshes_past_the_32bit_offset_limit():
+    """gnot_plan_set_batch bounds the points per plan so every [rows, 3d] activation stays addressable
+    by the kernels' 32-bit buffer offsets (gnot_hip.h: 0xFFFFFFFF / (12 d); d = 256 -> 1,398,101)."""
+    from gnot_amd import _lib
+    lib = _lib.load()
+    cfg = _lib.GnotConfig(input_dim=3, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=1,
+                          n_attn_hidden_dim=256, n_mlp_num_layers=4, n_mlp_hidden_dim=256, n_input_hidden_dim=256,
+                          n_expert=8, n_head=8, n_input_functions=1)
+    plan = ctypes.c_void_p()
+    _lib.check(lib.gnot_plan_create(ctypes.byref(cfg), ctypes.byref(plan)))
+    try:
+        lim = 0xFFFFFFFF // (12 * 256)
+        assert lim == 1398101
+        fo = (ctypes.c_int64 * 2)(0, 805)
+        _lib.check(lib.gnot_plan_set_batch(plan, 1, (ctypes.c_int64 * 2)(0, lim), fo, 0))
+        assert lib.gnot_plan_set_batch(plan, 1, (ctypes.c_int64 * 2)(0, lim + 1), fo, 0) == -1
+        assert b"point-shard" in lib.gnot_last_error()
+        assert lib.gnot_plan_set_batch(plan, 1, (ctypes.c_int64 * 2)(0, 1000),
+                                       (ctypes.c_int64 * 2)(0, lim + 1), 0) == -1
+    finally:
+        lib.gnot_plan_destroy(plan)
+
+
 def test_forward_refuses_cpu_tensors():
     from gnot_amd import GNOT
     m = GNOT(2, 1, 3, 1, 1, 32, 2, 32, 32, 2, 4, 0)
