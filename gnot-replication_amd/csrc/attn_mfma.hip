@@ -371,12 +371,19 @@ bool mfma_ok(const AttnApplyArgs& a, bool bwd) {
          (!bwd || ((a.lddq & 3) == 0 && (a.lddu & 3) == 0)) && apply_lds_bytes<DH>(a.nsrc, a.H, bwd) <= kApplyLdsMax;
 }
 
+// the dynamic-LDS cap of a kernel, raised ONCE to the largest size any launch may ask for (it is a cap
+// only: occupancy follows each launch's own size), not per launch
+static void allow_max_lds(const void* f) { (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kApplyLdsMax); }
+
 template <int DH, bool BWD>
 hipError_t launch_mfma(const AttnApplyArgs& a, hipStream_t s) {
   const size_t lds = apply_lds_bytes<DH>(a.nsrc, a.H, BWD);
-  const void* f = BWD ? reinterpret_cast<const void*>(attn_apply_bwd_mfma_kernel<DH>)
-                      : reinterpret_cast<const void*>(attn_apply_fwd_mfma_kernel<DH>);
-  if (lds > 64 * 1024) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  static const bool attr = [] {
+    allow_max_lds(BWD ? reinterpret_cast<const void*>(attn_apply_bwd_mfma_kernel<DH>)
+                      : reinterpret_cast<const void*>(attn_apply_fwd_mfma_kernel<DH>));
+    return true;
+  }();
+  (void)attr;
   const dim3 grid((a.nchunks + kApplyCpw - 1) / kApplyCpw), block(256);
   if (BWD) hipLaunchKernelGGL(attn_apply_bwd_mfma_kernel<DH>, grid, block, lds, s, a, kApplyCpw);
   else hipLaunchKernelGGL(attn_apply_fwd_mfma_kernel<DH>, grid, block, lds, s, a, kApplyCpw);
@@ -401,9 +408,12 @@ template <int DH>
 hipError_t launch_kv(const AttnKVBwdArgs* a, const AttnKVBwdArgs* jobs_dev, int njobs, int maxchunks, int H,
                      hipStream_t s) {
   const size_t lds = apply_lds_bytes<DH>(1, H, true);
-  const void* f = a ? reinterpret_cast<const void*>(attn_kv_bwd_mfma_kernel<DH>)
-                    : reinterpret_cast<const void*>(attn_kv_bwd_batch_mfma_kernel<DH>);
-  if (lds > 64 * 1024) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  static const bool attr = [] {
+    allow_max_lds(reinterpret_cast<const void*>(attn_kv_bwd_mfma_kernel<DH>));
+    allow_max_lds(reinterpret_cast<const void*>(attn_kv_bwd_batch_mfma_kernel<DH>));
+    return true;
+  }();
+  (void)attr;
   const int nch = a ? a->nchunks : maxchunks;
   const dim3 grid((nch + kApplyCpw - 1) / kApplyCpw, 1, a ? 1 : njobs), block(256);
   if (a) hipLaunchKernelGGL(attn_kv_bwd_mfma_kernel<DH>, grid, block, lds, s, *a, kApplyCpw);
