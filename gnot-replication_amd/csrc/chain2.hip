@@ -167,7 +167,12 @@ GNOT_DEV void c2f_layer(C2Pipe& pp, const u32x4* W, const u32x4 (&in)[KBI][NP], 
   epi(OT - 1, prev);
 }
 
-template <int D, int KT0, int OTL, bool SAVE, int NP>
+// WALK (CH_MOE only): the workgroup runs experts 0 .. E-1 of its 128 points one after the other and
+// sums in place, Y = base + sum_e s_e y_e: expert 0 reads the residual, expert e > 0 reads back the
+// partial sum this same lane stored for expert e-1 (same rows, same features), so no [P, E, d] stage
+// and no combine pass exist (model.py:128-131).  Every expert restarts the weight stream after a
+// barrier (its last layer issues no DMA).
+template <int D, int KT0, int OTL, bool SAVE, int NP, bool WALK>
 __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) {
   constexpr int DT = D / 16, KB = DT / 2, KB0 = (KT0 + 1) / 2;
   using LD = C2Lds<D, NP>;
@@ -175,23 +180,29 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) 
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4;
   const long p = ((long)blockIdx.x * kC2Waves + wave) * 16 + (lane & 15);
   const bool valid = p < a.P;
-  const int e = blockIdx.y, nl = a.nlin;
-  const ChainLayer* L = a.layers + e * nl;
-  float* save = SAVE ? a.save + e * a.save_chain_stride : nullptr;
+  const int nl = a.nlin;
   const unsigned lay_bytes = (unsigned)min((long)a.P * D * 4, 0xFFFFFFFFL);   // one [P, D] layer
   // byte offset of this lane's row in a [P, D] layer: unsigned (the plan bounds P * D * 4 < 2^32)
   const int voff = (int)(((unsigned)(blockIdx.x * kC2Waves + wave) * 16u + (unsigned)(lane & 15)) * (unsigned)(D * 4) +
                          16u * (unsigned)g);
   C2Pipe pp{c2lds, LD::WB, 0, wave, lane};
-  const u32x4* W0 = reinterpret_cast<const u32x4*>(L[0].Wp);
-  if (wave == 0) dma16(make_rsrc(L[0].bias, 16 * DT * 4), c2lds + LD::kBias, lane * 16, 0);
   constexpr int CH = c2f_pair<NP>() ? 2 : 1;         // output tiles per weight chunk
-  dma_image(c2lds, W0, CH * c2_tile_u4(KB0, NP), kC2Waves, wave, lane);
-  auto wp = [&](int l) { return reinterpret_cast<const u32x4*>(L[l].Wp); };
-  auto rs = [&](int l) { return make_rsrc(SAVE ? save + l * a.save_layer_stride : nullptr, SAVE ? lay_bytes : 0u); };
   // a layer's first wait: the saves the previous layer issued after its last weight DMA (its last
   // tile's stream + the final epilogue; pair mode: its last pair's two tiles + the final epilogue)
   constexpr int pend_next = SAVE ? (CH == 2 ? 3 : 2) : 0;
+  constexpr int e_begin = 0;
+  auto expert = [&](int e) __attribute__((always_inline)) {
+  const ChainLayer* L = a.layers + e * nl;
+  float* save = SAVE ? a.save + e * a.save_chain_stride : nullptr;
+  if (WALK && e > e_begin) {
+    __syncthreads();            // every wave is done with the previous expert's chunks and bias
+    pp.cnt = 0;
+  }
+  const u32x4* W0 = reinterpret_cast<const u32x4*>(L[0].Wp);
+  if (wave == 0) dma16(make_rsrc(L[0].bias, 16 * DT * 4), c2lds + LD::kBias, lane * 16, 0);
+  dma_image(c2lds, W0, CH * c2_tile_u4(KB0, NP), kC2Waves, wave, lane);
+  auto wp = [&](int l) { return reinterpret_cast<const u32x4*>(L[l].Wp); };
+  auto rs = [&](int l) { return make_rsrc(SAVE ? save + l * a.save_layer_stride : nullptr, SAVE ? lay_bytes : 0u); };
 
   float nx[DT][4];                                   // next layer input (fp32), then split
   u32x4 bp[KB][NP];
@@ -219,6 +230,32 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) 
   c2_split<DT, NP>(nx, bp);
   c2f_layer<OTL, KB, false, SAVE, NP>(pp, wp(nl - 1), bp, bsel, rs(nl - 1), voff, nullptr, 0, nullptr, 0, pend_next, g,
                                       y);
+  if constexpr (WALK) {
+    // Y = base + sum_e s_e y_e, accumulated in place in expert order (Y == nullptr: MoE recompute, saves only)
+    if (a.Y != nullptr) {
+      const float s = valid ? a.scores[p * a.ldsc + e] : 0.f;
+      const float* src = e == e_begin ? a.base : a.Y;
+      float acc[OTL][4];
+      if (src != nullptr) {
+        load_rows<OTL>(acc, src, a.ldy, p, valid, a.out_dim, lane);
+      } else {
+#pragma unroll
+        for (int T = 0; T < OTL; ++T)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[T][r] = 0.f;
+      }
+#pragma unroll
+      for (int T = 0; T < OTL; ++T)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          // the product rounded on its own (no FMA contraction): the expert grid's s_e * y_e store + add
+          float t = s * y[T][r];
+          asm volatile("" : "+v"(t));
+          y[T][r] = acc[T][r] + t;
+        }
+      store_rows<OTL>(y, a.Y, a.ldy, p, valid, a.out_dim, lane);
+    }
+  } else {
   if (a.mode == CH_SOFTMAX) {
     // softmax over the first out_dim outputs (features 16T + 4g + r); padded features excluded
     float m = -INFINITY;
@@ -253,6 +290,13 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) 
       for (int r = 0; r < 4; ++r) y[T][r] *= s;
   }
   store_rows<OTL>(y, a.Y + e * a.y_chain_stride, a.ldy, p, valid, a.out_dim, lane);
+  }
+  };
+  if constexpr (WALK) {
+    for (int e = 0; e < a.nchains; ++e) expert(e);
+  } else {
+    expert((int)blockIdx.y);
+  }
 }
 
 // ------------------------------------------------------------------------------------------ backward
@@ -326,7 +370,9 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP],
   stores(DT - 1);
 }
 
-template <int D, int KT0, int OTL, int NP>
+// WALK (CH_MOE only): experts 0 .. E-1 of the workgroup's points in order; dX = sum_e W_e0^T dz_e0 summed
+// in place (expert e > 0 reads back the partial this lane stored for e-1), no stage, no combine pass.
+template <int D, int KT0, int OTL, int NP, bool WALK>
 __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) {
   constexpr int DT = D / 16, KB = DT / 2, KBL = (OTL + 1) / 2;
   using LD = C2Lds<D, NP>;
@@ -334,15 +380,21 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) 
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4;
   const long p = ((long)blockIdx.x * kC2Waves + wave) * 16 + (lane & 15);
   const bool valid = p < a.P;
-  const int e = blockIdx.y, nl = a.nlin;
-  const ChainLayer* L = a.layers + e * nl;
-  const float* save = a.save + e * a.save_chain_stride;
-  float* dz = a.dz + e * a.dz_chain_stride;
+  const int nl = a.nlin;
   const unsigned lay_bytes = (unsigned)min((long)a.P * D * 4, 0xFFFFFFFFL);   // one [P, D] layer
   // byte offset of this lane's row in a [P, D] layer: unsigned (the plan bounds P * D * 4 < 2^32)
   const int voff = (int)(((unsigned)(blockIdx.x * kC2Waves + wave) * 16u + (unsigned)(lane & 15)) * (unsigned)(D * 4) +
                          16u * (unsigned)g);
   C2Pipe pp{c2lds, LD::WB, 0, wave, lane};
+  constexpr int e_begin = 0;
+  auto expert = [&](int e) __attribute__((always_inline)) {
+  const ChainLayer* L = a.layers + e * nl;
+  const float* save = a.save + e * a.save_chain_stride;
+  float* dz = a.dz + e * a.dz_chain_stride;
+  if (WALK && e > e_begin) {
+    __syncthreads();            // every wave is done with the previous expert's chunks and slots
+    pp.cnt = 0;
+  }
   auto wt = [&](int l) { return reinterpret_cast<const u32x4*>(L[l].WpT); };
   auto rh = [&](int l) { return make_rsrc(save + l * a.save_layer_stride, lay_bytes); };   // h_l
   auto rz = [&](int l) { return make_rsrc(dz + l * a.dz_layer_stride, lay_bytes); };      // dz_l
@@ -431,30 +483,69 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) 
 #pragma unroll
       for (int r = 0; r < 4; ++r) dx[o][r] = acc[r];
     }
-    store_rows<KT0>(dx, a.dX + e * a.dx_chain_stride, a.lddx, p, valid, a.in_dim, lane);
+    if constexpr (WALK) {
+      if (e > e_begin) {
+        float part[KT0][4];
+        load_rows<KT0>(part, a.dX, a.lddx, p, valid, a.in_dim, lane);
+#pragma unroll
+        for (int T = 0; T < KT0; ++T)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) dx[T][r] += part[T][r];
+      }
+      store_rows<KT0>(dx, a.dX, a.lddx, p, valid, a.in_dim, lane);
+    } else {
+      store_rows<KT0>(dx, a.dX + e * a.dx_chain_stride, a.lddx, p, valid, a.in_dim, lane);
+    }
+  }
+  };
+  if constexpr (WALK) {
+    for (int e = 0; e < a.nchains; ++e) expert(e);
+  } else {
+    expert((int)blockIdx.y);
   }
 }
 
 template <int D, int NP>
 static hipError_t launch_chain2_d(const ChainArgs& a, bool bwd, hipStream_t s) {
   constexpr int DT = D / 16;
-  const dim3 grid((a.P + 16 * kC2Waves - 1) / (16 * kC2Waves), a.nchains), block(64 * kC2Waves);
+  const dim3 grid((a.P + 16 * kC2Waves - 1) / (16 * kC2Waves), a.walk ? 1 : a.nchains), block(64 * kC2Waves);
   const size_t lds = C2Lds<D, NP>::kBytes;
-#define GNOT_C2_CASE(K0, OL)                                                                             \
-  if (a.KT0 == K0 && a.OTL == OL) {                                                                      \
+#define GNOT_C2_ATTR(K)                                                                                  \
+  do {                                                                                                   \
     static bool attr = false;                                                                            \
     if (!attr) {                                                                                         \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(chain2_bwd_kernel<D, K0, OL, NP>),         \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                   \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(chain2_fwd_kernel<D, K0, OL, true, NP>),   \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                   \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(chain2_fwd_kernel<D, K0, OL, false, NP>),  \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                   \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(K), hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                (int)lds);                                                               \
       attr = true;                                                                                       \
     }                                                                                                    \
-    if (bwd) hipLaunchKernelGGL((chain2_bwd_kernel<D, K0, OL, NP>), grid, block, lds, s, a);             \
-    else if (a.save) hipLaunchKernelGGL((chain2_fwd_kernel<D, K0, OL, true, NP>), grid, block, lds, s, a); \
-    else hipLaunchKernelGGL((chain2_fwd_kernel<D, K0, OL, false, NP>), grid, block, lds, s, a);          \
+  } while (0)
+  if (a.walk) {
+    // the walk form exists for the soft-MoE experts (d x d chains) only
+    if (a.mode != CH_MOE || a.KT0 != DT || a.OTL != DT) return hipErrorInvalidValue;
+    if (bwd) {
+      GNOT_C2_ATTR((chain2_bwd_kernel<D, DT, DT, NP, true>));
+      hipLaunchKernelGGL((chain2_bwd_kernel<D, DT, DT, NP, true>), grid, block, lds, s, a);
+    } else if (a.save) {
+      GNOT_C2_ATTR((chain2_fwd_kernel<D, DT, DT, true, NP, true>));
+      hipLaunchKernelGGL((chain2_fwd_kernel<D, DT, DT, true, NP, true>), grid, block, lds, s, a);
+    } else {
+      GNOT_C2_ATTR((chain2_fwd_kernel<D, DT, DT, false, NP, true>));
+      hipLaunchKernelGGL((chain2_fwd_kernel<D, DT, DT, false, NP, true>), grid, block, lds, s, a);
+    }
+    return hipGetLastError();
+  }
+#define GNOT_C2_CASE(K0, OL)                                                                             \
+  if (a.KT0 == K0 && a.OTL == OL) {                                                                      \
+    if (bwd) {                                                                                           \
+      GNOT_C2_ATTR((chain2_bwd_kernel<D, K0, OL, NP, false>));                                           \
+      hipLaunchKernelGGL((chain2_bwd_kernel<D, K0, OL, NP, false>), grid, block, lds, s, a);             \
+    } else if (a.save) {                                                                                 \
+      GNOT_C2_ATTR((chain2_fwd_kernel<D, K0, OL, true, NP, false>));                                     \
+      hipLaunchKernelGGL((chain2_fwd_kernel<D, K0, OL, true, NP, false>), grid, block, lds, s, a);       \
+    } else {                                                                                             \
+      GNOT_C2_ATTR((chain2_fwd_kernel<D, K0, OL, false, NP, false>));                                    \
+      hipLaunchKernelGGL((chain2_fwd_kernel<D, K0, OL, false, NP, false>), grid, block, lds, s, a);      \
+    }                                                                                                    \
     return hipGetLastError();                                                                            \
   }
   GNOT_C2_CASE(1, 1)
@@ -462,7 +553,31 @@ static hipError_t launch_chain2_d(const ChainArgs& a, bool bwd, hipStream_t s) {
   GNOT_C2_CASE(DT, 1)
   GNOT_C2_CASE(DT, DT)
 #undef GNOT_C2_CASE
+#undef GNOT_C2_ATTR
   return hipErrorInvalidValue;
+}
+
+// Walk form or one workgroup per (point block, expert): the walk form has E x fewer, E x longer
+// workgroups (one per CU: 82 KiB LDS), so its last round of workgroups can leave CUs idle where the
+// expert grid fills them; the expert grid pays the [P, E, d] stage and the combine pass instead
+// (~7 % of the MoE forward at configs[2]).  Walk when its CU-round efficiency is within 10 % of the
+// expert grid's.  env GNOT_MOE_WALK = 0 / 1 forces either (read per call: the tests run both).
+bool chain2_walk_choice(long P, int E) {
+  if (const char* env = std::getenv("GNOT_MOE_WALK")) {
+    if (env[0] == '0') return false;
+    if (env[0] == '1') return true;
+  }
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  if (E < 2) return false;
+  const long blk = (P + 16 * kC2Waves - 1) / (16 * kC2Waves);
+  auto eff = [&](long wgs) { return (double)wgs / (double)(((wgs + cus - 1) / cus) * cus); };
+  return eff(blk) >= 0.9 * eff(blk * E);
 }
 
 hipError_t launch_chain2(const ChainArgs& a, bool bwd, hipStream_t s) {

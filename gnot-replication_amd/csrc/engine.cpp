@@ -183,6 +183,9 @@ struct gnot_plan {
   // input; the backward re-runs that call's expert forward into ONE shared save buffer ("mrsave")
   // just before its chain backward -- E*NL*P*D floats once instead of per MoE call
   bool moe_recompute = false;
+  // soft-MoE calls in the walk form (chain2.hip: one workgroup sums all experts in place, no [P, E, d]
+  // stage): decided per batch in gnot_plan_set_batch (chain2_walk_choice)
+  bool moe_walk = false;
   // operand pieces of the d = 256 bf16-MFMA kernels (chain2, linear2, wide weight gradients):
   // 3 = bf16x6 (fp32-exact, default), 1 = bf16 arithmetic mode (gnot_plan_set_precision)
   int np = 3;
@@ -1079,7 +1082,8 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
     if (tr && !p->moe_recompute) C.add(s + "m2save", E * NL * P * D, D);
     C.add(s + "query2", P * D, D);
   }
-  C.add("stage", E * P * D, D);
+  p->moe_walk = p->D == 256 && p->L > 0 && chain2_walk_choice(P, E);
+  if (!p->moe_walk) C.add("stage", E * P * D, D);
   if (tr && p->moe_recompute && p->L > 0) C.add("mrsave", E * NL * P * D, D);
   if (p->sharded) {                          // scramble exchange scratch: head-major rows / packed peers
     C.add("xa", P * D, D);
@@ -1624,6 +1628,31 @@ int attn_backward(Ctx& c, int l, bool cross) {
 
 }  // namespace
 
+// the soft-MoE experts of one call: walk form (d = 256, chain2.hip) or the expert grid + moe_combine
+static bool moe_walk(gnot_plan* p) { return p->moe_walk; }
+
+static int moe_forward(Ctx& c, const ChainTable& T, const float* in, const float* qin, float* qout, float* save) {
+  gnot_plan* p = c.p;
+  const long P = p->P;
+  const int D = p->D, E = p->E, NL = p->NL;
+  const bool walk = moe_walk(p);
+  ChainArgs a = chain_args(p, T, P);
+  a.X = in; a.ldx = D; a.ldy = D;
+  a.scores = p->P_("scores"); a.ldsc = (int)p->bufs["scores"].ld; a.mode = CH_MOE;
+  if (save) { a.save = save; a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D; }
+  if (walk) {
+    a.walk = 1; a.Y = qout; a.base = qin;
+  } else {
+    a.Y = p->P_("stage"); a.y_chain_stride = P * D;
+  }
+  {
+    ProfScope ps(c, "moe_fwd", 2.0 * E * P * NL * (double)D * D);
+    GNOT_CK(launch_chain_fwd(a, c.s));
+  }
+  if (!walk) GNOT_CK(launch_moe_combine(qin, p->P_("stage"), P * D, E, qout, P * D, c.s));
+  return GNOT_OK;
+}
+
 extern "C" int gnot_forward(gnot_plan* p, const float* x, const float* theta, const float* const* fns,
                             float* out, void* stream) {
   if (!p || !p->ws_bound) return fail(GNOT_E_STATE, "bind_workspace first");
@@ -1631,7 +1660,7 @@ extern "C" int gnot_forward(gnot_plan* p, const float* x, const float* theta, co
   if (!x || !theta || !out || (p->I > 0 && !fns)) return fail(GNOT_E_INVALID, "null input");
   Ctx c{p, static_cast<hipStream_t>(stream)};
   const long P = p->P;
-  const int D = p->D, E = p->E, NL = p->NL;
+  const int D = p->D, NL = p->NL;
   const bool tr = p->training;
   // the input-function branch (encoders, every block's K/V projections and states) depends only on
   // the input functions: it runs on side2 while the query branch (gating, x encoder) runs here.  The
@@ -1698,33 +1727,13 @@ extern "C" int gnot_forward(gnot_plan* p, const float* x, const float* theta, co
     const std::string s = "b" + std::to_string(l) + ".";
     const float* qin = p->P_(p->block_query(l));
     GNOT_RUN(attn_forward(c, l, true, qin, p->P_(s + "cres"), p->P_(s + "a")));
-    {
-      ChainArgs a = chain_args(p, p->ch_m1[l], P);
-      a.X = p->P_(s + "a"); a.ldx = D; a.Y = p->P_("stage"); a.ldy = D; a.y_chain_stride = P * D;
-      a.scores = p->P_("scores"); a.ldsc = (int)p->bufs["scores"].ld; a.mode = CH_MOE;
-      if (tr && !p->moe_recompute) {
-        a.save = p->P_(s + "m1save"); a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D;
-      }
-      {
-        ProfScope ps(c, "moe_fwd", 2.0 * E * P * NL * (double)D * D);
-        GNOT_CK(launch_chain_fwd(a, c.s));
-      }
-      GNOT_CK(launch_moe_combine(qin, p->P_("stage"), P * D, E, p->P_(s + "query1"), P * D, c.s));
-    }
+    // ffn1 experts: query1 = query + sum_e s_e ffn1_e(a)   (model.py:128-131)
+    GNOT_RUN(moe_forward(c, p->ch_m1[l], p->P_(s + "a"), qin, p->P_(s + "query1"),
+                         tr && !p->moe_recompute ? p->P_(s + "m1save") : nullptr));
     GNOT_RUN(attn_forward(c, l, false, p->P_(s + "query1"), p->P_(s + "sres"), p->P_(s + "bb")));
-    {
-      ChainArgs a = chain_args(p, p->ch_m2[l], P);
-      a.X = p->P_(s + "bb"); a.ldx = D; a.Y = p->P_("stage"); a.ldy = D; a.y_chain_stride = P * D;
-      a.scores = p->P_("scores"); a.ldsc = (int)p->bufs["scores"].ld; a.mode = CH_MOE;
-      if (tr && !p->moe_recompute) {
-        a.save = p->P_(s + "m2save"); a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D;
-      }
-      {
-        ProfScope ps(c, "moe_fwd", 2.0 * E * P * NL * (double)D * D);
-        GNOT_CK(launch_chain_fwd(a, c.s));
-      }
-      GNOT_CK(launch_moe_combine(p->P_(s + "query1"), p->P_("stage"), P * D, E, p->P_(s + "query2"), P * D, c.s));
-    }
+    // ffn2 experts: query2 = query1 + sum_e s_e ffn2_e(bb)   (model.py:134-137)
+    GNOT_RUN(moe_forward(c, p->ch_m2[l], p->P_(s + "bb"), p->P_(s + "query1"), p->P_(s + "query2"),
+                         tr && !p->moe_recompute ? p->P_(s + "m2save") : nullptr));
   }
   // decoder (model.py:171)
   {
@@ -1745,7 +1754,7 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
   const long P = p->P;
   const int D = p->D, E = p->E, NL = p->NL;
   float* dquery = p->P_("dquery");
-  float* stage = p->P_("stage");
+  float* stage = p->moe_walk ? nullptr : p->P_("stage");
   p->readers.clear();
   GNOT_CK(hipMemcpy2DAsync(p->P_("dout"), p->bufs["dout"].ld * 4, dout, p->out * 4, p->out * 4, P,
                            hipMemcpyDeviceToDevice, c.s));
@@ -1761,8 +1770,13 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
       GNOT_CK(launch_chain_bwd(a, cc.s));
     }
     // the weight gradients read the saved pre-activations too: a recomputed (shared) save buffer
-    // must not be overwritten by the next MoE's recompute before they finish
-    if (p->moe_recompute && a.mode == CH_MOE) return run_wgrad_side(cc, G, {dz, a.save});
+    // must not be overwritten by the next MoE's recompute before they finish.  That guard is the
+    // readers map, which only run_wgrad_side from the capture-origin stream registers (side2 runs its
+    // groups in order without it): the MoE chains must therefore stay on the origin stream
+    if (p->moe_recompute && a.mode == CH_MOE) {
+      if (cc.s != c.s) return fail(GNOT_E_STATE, "internal: MoE recompute backward off the origin stream");
+      return run_wgrad_side(cc, G, {dz, a.save});
+    }
     return run_wgrad_side(cc, G, {dz});
   };
   auto chain_bwd = [&](ChainArgs& a, int kcall, long rows, const WgradGroup& G, const char* prof) -> int {
@@ -1776,6 +1790,7 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
     a.dX = dquery; a.lddx = D; a.dx_chain_stride = 0;
     GNOT_RUN(chain_bwd(a, p->k_out(), P, p->wg_out, "chain_bwd"));
   }
+  const bool walk = moe_walk(p);
   for (int l = p->L - 1; l >= 0; --l) {
     const std::string s = "b" + std::to_string(l) + ".";
     // ffn2 experts: query2 = query1 + sum_e s_e ffn2_e(bb)   (model.py:134-137)
@@ -1786,9 +1801,12 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
         float* mr = p->P_("mrsave");
         GNOT_RUN(guard_write(c, mr));
         ChainArgs f = chain_args(p, m1 ? p->ch_m1[l] : p->ch_m2[l], P);
-        f.X = p->P_(s + (m1 ? "a" : "bb")); f.ldx = D; f.Y = stage; f.ldy = D; f.y_chain_stride = P * D;
+        f.X = p->P_(s + (m1 ? "a" : "bb")); f.ldx = D; f.ldy = D;
         f.scores = p->P_("scores"); f.ldsc = (int)p->bufs["scores"].ld; f.mode = CH_MOE;
         f.save = mr; f.save_layer_stride = P * D; f.save_chain_stride = NL * P * D;
+        // only the saves are needed: the walk form writes no output (Y = null), the expert grid its stage
+        f.walk = walk ? 1 : 0;
+        f.Y = walk ? nullptr : stage; f.y_chain_stride = P * D;
         ProfScope ps(c, "moe_recompute", 2.0 * E * P * NL * (double)D * D);
         GNOT_CK(launch_chain_fwd(f, c.s));
       }
@@ -1796,11 +1814,19 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
       a.dY = dquery; a.lddy = D; a.mode = CH_MOE;
       a.scores = p->P_("scores"); a.ldsc = (int)p->bufs["scores"].ld; a.dscore = p->P_("dscore");
       a.save = p->P_(p->msave(l, m1)); a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D;
-      a.dX = stage; a.lddx = D; a.dx_chain_stride = P * D;
-      GNOT_RUN(chain_bwd(a, m1 ? p->k_m1(l) : p->k_m2(l), P, m1 ? p->wg_m1[l] : p->wg_m2[l], "moe_bwd"));
       float* dsum = p->P_(p->dsum_buf(m1));
-      GNOT_RUN(guard_write(c, dsum));
-      GNOT_CK(launch_moe_combine(nullptr, stage, P * D, E, dsum, P * D, c.s));
+      if (walk) {
+        // d(MoE input) = sum_e W_e0^T dz_e0 summed in place by the walk form (no stage, no combine)
+        GNOT_RUN(guard_write(c, dsum));
+        a.walk = 1; a.dX = dsum; a.lddx = D; a.dx_chain_stride = 0;
+      } else {
+        a.dX = stage; a.lddx = D; a.dx_chain_stride = P * D;
+      }
+      GNOT_RUN(chain_bwd(a, m1 ? p->k_m1(l) : p->k_m2(l), P, m1 ? p->wg_m1[l] : p->wg_m2[l], "moe_bwd"));
+      if (!walk) {
+        GNOT_RUN(guard_write(c, dsum));
+        GNOT_CK(launch_moe_combine(nullptr, stage, P * D, E, dsum, P * D, c.s));
+      }
       // m2: self attention (model.py:133) ; m1: cross attention (model.py:127)
       GNOT_RUN(attn_backward(c, l, m1));
     }

@@ -86,7 +86,15 @@ struct ChainArgs {
   float* dz; long dz_layer_stride; long dz_chain_stride;          // per layer dZ [P, D] for wgrad
   float* dX; long lddx; long dx_chain_stride;                     // chain input grad or null
   int np = 3;                        // d = 256: operand pieces (3 = bf16x6 fp32-exact, 1 = bf16 mode)
+  // CH_MOE, d = 256 (chain2.hip) "walk" form: ONE workgroup runs every expert of its 128 points in
+  // order and sums in place -- forward Y = base + sum_e s_e * MLP_e(X) (model.py:128-131), backward
+  // dX = sum_e W_e0^T dz_e0 -- so no [P, E, d] stage and no combine pass (grid.y = 1).  Forward Y may
+  // be null (MoE recompute: saves only).
+  int walk = 0;
+  const float* base = nullptr;       // walk forward: the residual (query in); null = 0
 };
+// walk or per-expert grid for a MoE call of P points (env GNOT_MOE_WALK = 0 / 1 forces, read per call)
+bool chain2_walk_choice(long P, int E);
 hipError_t launch_chain_fwd(const ChainArgs& a, hipStream_t s);
 hipError_t launch_chain_bwd(const ChainArgs& a, hipStream_t s);
 // d = 256 chains (chain2.hip): bf16x6 in both directions, output-major x6 images (pack x6 = 2) for Wp

@@ -14,6 +14,8 @@ the 262,144-point bench takes:
   256 workgroups: 6 splits per MoE job group of 40 Linears, 51 per single-chain group of 5), and an
   odd number of 16-point stages in the last split (70,000 - 5 * 11,680 = 11,600 points = 725
   stages), the case of the stage-buffer reuse the db column sums once raced on;
+* the soft-MoE walk form (forced: GNOT_MOE_WALK=1; the bench's 262,144 points select it
+  automatically) and the expert grid;
 * 70,000 is not a multiple of 128 (a partial last chain workgroup) nor of 256 (a partial state block).
 
 Checked against the float64 CPU oracle (oracle/gnot_oracle.py, pinned to the reference fixtures):
@@ -46,14 +48,18 @@ def mid_case():
 
 
 @pytest.mark.timeout(900)
-def test_configs2_widths_70k_points_fp32(mid_case):
+@pytest.mark.parametrize("walk", ["1", "0"])
+def test_configs2_widths_70k_points_fp32(mid_case, walk, monkeypatch):
+    """walk "1": the soft-MoE walk form the 262,144-point bench selects (at 70,000 points the automatic
+    choice is the expert grid, chain2_walk_choice); "0": the expert grid + moe_combine."""
+    monkeypatch.setenv("GNOT_MOE_WALK", walk)
     fx, G = mid_case
     m = build_model(fx["params"], fx["cfg"])
     out, grads = run_packed(m, fx, G)
     errs = check_parity(out, grads, fx)
     keys = sorted(fx["grads"])
     cat = lambda g: np.concatenate([np.ravel(g[k]) for k in keys])
-    print(f"\n70k fp32: out rel {rel(out, fx['out']):.3e}, all-grad rel {rel(cat(grads), cat(fx['grads'])):.3e}")
+    print(f"\n70k fp32 walk={walk}: out rel {rel(out, fx['out']):.3e}, all-grad rel {rel(cat(grads), cat(fx['grads'])):.3e}")
     assert not errs, errs
     out2, grads2 = run_packed(m, fx, G)
     assert np.array_equal(out, out2)
@@ -62,7 +68,8 @@ def test_configs2_widths_70k_points_fp32(mid_case):
 
 
 @pytest.mark.timeout(900)
-def test_configs2_widths_70k_points_bf16_mode(mid_case):
+def test_configs2_widths_70k_points_bf16_mode(mid_case, monkeypatch):
+    monkeypatch.setenv("GNOT_MOE_WALK", "1")       # the headline's soft-MoE form
     fx, G = mid_case
     m = build_model(fx["params"], fx["cfg"])
     m.set_precision("bf16")
