@@ -282,7 +282,8 @@ def main():
     ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32",
                     help="fp32: the reference's arithmetic (bf16x6-exact MFMA); bf16: configs[2]'s bf16 training "
                          "(one RNE bf16 operand per MFMA in the d=256 chains / projections / weight gradients, "
-                         "fp32 accumulation and storage; north_star's 1e-2 bar, tests/test_gpu_bf16.py)")
+                         "fp32 accumulation; the soft-MoE chains keep their saves, dZ and Linear inputs in bf16; "
+                         "north_star's 1e-2 bar, tests/test_gpu_bf16.py)")
     ap.add_argument("--fp32-only", action="store_true",
                     help="skip the companion bf16-mode measurement of the default fp32 run (configs[2], N=1)")
     ap.add_argument("--recompute", choices=["auto", "on", "off"], default="auto",
@@ -576,7 +577,8 @@ def main():
             "ms_per_step": round(M1["elapsed"] / args.steps * 1e3, 4),
             "dtype": "bf16",
             "arithmetic": "one RNE bf16 operand per MFMA in the d=256 chains / projections / weight gradients, "
-                          "fp32 accumulation and storage (GNOT.set_precision('bf16'); tests/test_gpu_bf16.py: "
+                          "fp32 accumulation; bf16 storage of the soft-MoE chains' saves, dZ and Linear inputs "
+                          "(GNOT.set_precision('bf16'); tests/test_gpu_bf16.py: "
                           "1e-2 of the fp64 oracle)",
             "roofline": roofline(M1, "bf16"),
         }

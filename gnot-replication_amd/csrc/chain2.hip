@@ -66,24 +66,49 @@ struct C2Lds {
 // + barrier, DMA of tile o+1 (or of the next layer's bias then tile 0), the 6 x KB MFMAs, then the
 // epilogue of tile o-1 (its save store is the ONLY vector-memory op after the DMA, so the next wait is
 // vmcnt(1)).
-template <int OT, int KBI, bool GELU, bool SAVE, int NP>
+// B16: the save is the RNE bf16 tile at its pair-interleaved position (voff = the lane's row * 512 B)
+template <int OT, int KBI, bool GELU, bool SAVE, int NP, bool B16 = false>
 GNOT_DEV void c2f_layer(C2Pipe& pp, const u32x4* W, const u32x4 (&in)[KBI][NP], int bsel, rsrc_t rs, int voff,
                         const u32x4* nextW, int next_n16, const float* next_bias, int next_bias_bytes, int pend0,
                         int g, float (&out)[OT][4]) {
   constexpr int TU = c2_tile_u4(KBI, NP);
   const u32x4* bias = pp.lds + C2Lds<256, NP>::kBias + bsel * 64;
   f32x4 prev;
-  auto epi = [&](int o, const f32x4& acc) {
-    if (SAVE) buf_store_f32x4(make_float4(acc[0], acc[1], acc[2], acc[3]), rs, voff + 64 * o);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) out[o][r] = GELU ? gelu(acc[r]) : acc[r];
-    pin4(out[o]);
+  auto save_tile = [&](int o, const f32x4& acc) {
+    if constexpr (B16) {
+      const float v[4] = {acc[0], acc[1], acc[2], acc[3]};
+      store_tile_b16(v, rs, voff, o, g);
+    } else {
+      buf_store_f32x4(make_float4(acc[0], acc[1], acc[2], acc[3]), rs, voff + 64 * o);
+    }
   };
-  // one part of tile o's epilogue (inside the next tile's MFMA stream): part 0 the save store
+  // B16 GELU layers save gelu'(h) instead of h (bf16 mode: the backward then multiplies instead of
+  // evaluating gelu', and the weight gradients read the stored Linear inputs, not h), from the same tail
+  // evaluation as gelu(h); stored after the tile's last value
+  constexpr bool SGRAD = B16 && GELU;
+  float gd[4];
+  auto epi = [&](int o, const f32x4& acc) {
+    if (SAVE && !SGRAD) save_tile(o, acc);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if constexpr (SGRAD) out[o][r] = gelu_and_grad(acc[r], gd[r]);
+      else out[o][r] = GELU ? gelu(acc[r]) : acc[r];
+    }
+    pin4(out[o]);
+    if (SAVE && SGRAD) save_tile(o, f32x4{gd[0], gd[1], gd[2], gd[3]});
+  };
+  // one part of tile o's epilogue (inside the next tile's MFMA stream): part 0 the save store (SGRAD:
+  // part 3)
   auto epi_part = [&](int o, const f32x4& acc, int r) {
-    if (SAVE && r == 0) buf_store_f32x4(make_float4(acc[0], acc[1], acc[2], acc[3]), rs, voff + 64 * o);
-    out[o][r] = GELU ? gelu(acc[r]) : acc[r];
-    asm volatile("" : "+v"(out[o][r]));
+    if (SAVE && !SGRAD && r == 0) save_tile(o, acc);
+    if constexpr (SGRAD) {
+      out[o][r] = gelu_and_grad(acc[r], gd[r]);
+      asm volatile("" : "+v"(out[o][r]), "+v"(gd[r]));
+      if (SAVE && r == 3) save_tile(o, f32x4{gd[0], gd[1], gd[2], gd[3]});
+    } else {
+      out[o][r] = GELU ? gelu(acc[r]) : acc[r];
+      asm volatile("" : "+v"(out[o][r]));
+    }
   };
   if constexpr (c2f_pair<NP>()) {
   // pair mode: one chunk = tiles o, o+1; the wait at pair o retires the DMA issued at pair o-2, after
@@ -172,7 +197,9 @@ GNOT_DEV void c2f_layer(C2Pipe& pp, const u32x4* W, const u32x4 (&in)[KBI][NP], 
 // partial sum this same lane stored for expert e-1 (same rows, same features), so no [P, E, d] stage
 // and no combine pass exist (model.py:128-131).  Every expert restarts the weight stream after a
 // barrier (its last layer issues no DMA).
-template <int D, int KT0, int OTL, bool SAVE, int NP, bool WALK>
+// B16 (bf16 mode, ChainArgs::b16s): bf16 pair-interleaved saves, plus each Linear's RNE bf16 input (the
+// split the MFMAs consume, stored as it is made) for the weight gradients
+template <int D, int KT0, int OTL, bool SAVE, int NP, bool WALK, bool B16 = false>
 __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) {
   constexpr int DT = D / 16, KB = DT / 2, KB0 = (KT0 + 1) / 2;
   using LD = C2Lds<D, NP>;
@@ -185,6 +212,9 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) 
   // byte offset of this lane's row in a [P, D] layer: unsigned (the plan bounds P * D * 4 < 2^32)
   const int voff = (int)(((unsigned)(blockIdx.x * kC2Waves + wave) * 16u + (unsigned)(lane & 15)) * (unsigned)(D * 4) +
                          16u * (unsigned)g);
+  // B16: this lane's row in the bf16 layers (512 B per point; the plan bounds P * 512 < 2^32)
+  const int rowb = (int)(((unsigned)(blockIdx.x * kC2Waves + wave) * 16u + (unsigned)(lane & 15)) * (unsigned)kB16Row);
+  const unsigned lay_b16 = (unsigned)min((long)a.P * kB16Row, 0xFFFFFFFFL);
   C2Pipe pp{c2lds, LD::WB, 0, wave, lane};
   constexpr int CH = c2f_pair<NP>() ? 2 : 1;         // output tiles per weight chunk
   // a layer's first wait: the saves the previous layer issued after its last weight DMA (its last
@@ -202,7 +232,18 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) 
   if (wave == 0) dma16(make_rsrc(L[0].bias, 16 * DT * 4), c2lds + LD::kBias, lane * 16, 0);
   dma_image(c2lds, W0, CH * c2_tile_u4(KB0, NP), kC2Waves, wave, lane);
   auto wp = [&](int l) { return reinterpret_cast<const u32x4*>(L[l].Wp); };
-  auto rs = [&](int l) { return make_rsrc(SAVE ? save + l * a.save_layer_stride : nullptr, SAVE ? lay_bytes : 0u); };
+  auto rs = [&](int l) {
+    return make_rsrc(SAVE ? save + l * a.save_layer_stride : nullptr, SAVE ? (B16 ? lay_b16 : lay_bytes) : 0u);
+  };
+  const int svoff = B16 ? rowb : voff;
+  // B16: a Linear's bf16 input words (k-blocks 0 .. nkb-1) into save slot `slot`; returns the stores issued
+  auto store_in = [&](const float* slot, const u32x4 (&w)[KB][NP], int nkb) __attribute__((always_inline)) {
+    const rsrc_t r = make_rsrc(slot, lay_b16);
+#pragma unroll
+    for (int t = 0; t < KB; ++t)
+      if (t < nkb) buf_store_b128(w[t][0], r, rowb + (t * 4 + g) * 16);
+    return nkb;
+  };
 
   float nx[DT][4];                                   // next layer input (fp32), then split
   u32x4 bp[KB][NP];
@@ -212,24 +253,33 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) 
     load_rows<KT0>(x0, a.X, a.ldx, p, valid, a.in_dim, lane);
     u32x4 b0[KB0][NP];
     c2_split<KT0, NP>(x0, b0);
+    int pend0 = 0;
+    if constexpr (B16) {
+      // the shared MoE input (Linear 0's operand): chain 0 only
+      if (WALK ? e == 0 : blockIdx.y == 0) {
+        if constexpr (KB0 == KB) pend0 = store_in(a.save + nl * a.save_layer_stride, b0, KB0);
+      }
+    }
     const int nb = nl - 1 == 1 ? 16 * OTL * 4 : 16 * DT * 4;
-    c2f_layer<DT, KB0, true, SAVE, NP>(pp, W0, b0, bsel, rs(0), voff, wp(1),
-                                       (nl - 1 == 1 ? (OTL < CH ? OTL : CH) : CH) * c2_tile_u4(KB, NP), L[1].bias, nb, 0,
-                                       g, nx);
+    c2f_layer<DT, KB0, true, SAVE, NP, B16>(pp, W0, b0, bsel, rs(0), svoff, wp(1),
+                                            (nl - 1 == 1 ? (OTL < CH ? OTL : CH) : CH) * c2_tile_u4(KB, NP), L[1].bias,
+                                            nb, pend0, g, nx);
     bsel ^= 1;
   }
   for (int l = 1; l < nl - 1; ++l) {
     c2_split<DT, NP>(nx, bp);
+    const int pin = B16 ? store_in(save + (nl + l) * a.save_layer_stride, bp, KB) : 0;
     const int nb = l + 1 == nl - 1 ? 16 * OTL * 4 : 16 * DT * 4;
-    c2f_layer<DT, KB, true, SAVE, NP>(pp, wp(l), bp, bsel, rs(l), voff, wp(l + 1),
-                                      (l + 1 == nl - 1 ? (OTL < CH ? OTL : CH) : CH) * c2_tile_u4(KB, NP),
-                                      L[l + 1].bias, nb, pend_next, g, nx);
+    c2f_layer<DT, KB, true, SAVE, NP, B16>(pp, wp(l), bp, bsel, rs(l), svoff, wp(l + 1),
+                                           (l + 1 == nl - 1 ? (OTL < CH ? OTL : CH) : CH) * c2_tile_u4(KB, NP),
+                                           L[l + 1].bias, nb, pend_next + pin, g, nx);
     bsel ^= 1;
   }
   float y[OTL][4];
   c2_split<DT, NP>(nx, bp);
-  c2f_layer<OTL, KB, false, SAVE, NP>(pp, wp(nl - 1), bp, bsel, rs(nl - 1), voff, nullptr, 0, nullptr, 0, pend_next, g,
-                                      y);
+  const int pin_last = B16 ? store_in(save + (2 * nl - 1) * a.save_layer_stride, bp, KB) : 0;
+  c2f_layer<OTL, KB, false, SAVE, NP, B16>(pp, wp(nl - 1), bp, bsel, rs(nl - 1), svoff, nullptr, 0, nullptr, 0,
+                                           pend_next + pin_last, g, y);
   if constexpr (WALK) {
     // Y = base + sum_e s_e y_e, accumulated in place in expert order (Y == nullptr: MoE recompute, saves only)
     if (a.Y != nullptr) {
@@ -305,33 +355,53 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) 
 // two tiles ahead into this wave's four slots (tile o in slot o % 4; the next layer's tiles 0 and 1
 // are requested by this layer's last two tiles).  Entry: the layer's tile-0 weights in pp.cur(), its
 // h tiles 0 and 1 requested, `pend0` vector-memory ops issued after its tile-0 weight DMA.
-template <int KBI, int NP>
+// B16 (bf16 storage, voff = the lane's row * 512 B): h and dz are pair-interleaved bf16 rows; one 16-byte
+// DMA brings the h of a tile PAIR (pair m into slot m % 4, requested at tile 2m - 2), dz stores are 8 B
+template <int KBI, int NP, bool B16 = false>
 GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP], rsrc_t rh, rsrc_t rz, rsrc_t rh_next,
                         bool has_next_h, int voff, const u32x4* nextW, int next_n16, int pend0, float (&nx)[16][4]) {
   constexpr int DT = 16, TU = c2_tile_u4(KBI, NP);
   u32x4* slots = pp.lds + C2Lds<256, NP>::kHs + pp.wave * 4 * 64;
+  const int g = pp.lane >> 4;
   f32x4 prev;
   // one part of tile o's epilogue (inside the next tile's MFMA stream): part 0 waits for the saved
   // pre-activation tile
   f32x4 hc;
+  u32x2 hb;
   auto epi_part = [&](int o, const f32x4& acc, int r) {
     // the saved tile was read at the top of this tile (lds_read16_issue); wait for it here
-    if (r == 0) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(hc) :: "memory");
-    nx[o][r] = acc[r] * gelu_grad(hc[r]);
+    float h;
+    if constexpr (B16) {
+      if (r == 0) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(hb) :: "memory");
+      h = (r & 1) ? bf16_hi(hb[r >> 1]) : bf16_lo(hb[r >> 1]);
+    } else {
+      if (r == 0) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(hc) :: "memory");
+      h = hc[r];
+    }
+    // B16: the forward stored gelu'(h_{l-1}) itself (c2f_layer SGRAD)
+    nx[o][r] = acc[r] * (B16 ? h : gelu_grad(h));
     asm volatile("" : "+v"(nx[o][r]));
+  };
+  // the saved tile of tile o's epilogue, read from its slot
+  auto read_h = [&](int o) {
+    if constexpr (B16) hb = lds_read8_issue(slots + ((o >> 1) & 3) * 64 + pp.lane, 8 * (o & 1));
+    else hc = lds_read16_issue(slots + (o & 3) * 64 + pp.lane);
   };
   // tile o's dz store is issued at the top of tile o+2, after that tile's DMAs: a counted wait only
   // retires the ops issued before the DMA it waits for, so each store gets two tiles to drain
   auto stores = [&](int o) {
-    buf_store_f32x4(make_float4(nx[o][0], nx[o][1], nx[o][2], nx[o][3]), rz, voff + 64 * o);
+    if constexpr (B16) store_tile_b16(nx[o], rz, voff, o, g);
+    else buf_store_f32x4(make_float4(nx[o][0], nx[o][1], nx[o][2], nx[o][3]), rz, voff + 64 * o);
   };
+  // does tile t request saved rows (fp32: tile t + 2; B16: at even t, pair t / 2 + 1)?
+  auto hdma = [&](int t) { return (!B16 || (t & 1) == 0) && (t + 2 < DT || has_next_h); };
   constexpr int S = 1;                                   // stores per tile
 #pragma unroll
   for (int o = 0; o < DT; ++o) {
     // ops issued after the weight DMA this wait retires (at the top of tile o-1): that tile's h DMA
     // (none when it would be past the next layer) and the stores of tile o-3
     if (o == 0) c2_sync_n(pend0);
-    else c2_sync_n(((o + 1 < DT || has_next_h) ? 1 : 0) + (o >= 3 ? S : 0));
+    else c2_sync_n((hdma(o - 1) ? 1 : 0) + (o >= 3 ? S : 0));
     const u32x4* cb = pp.cur();
     u32x4* nb = pp.nxt();
     ++pp.cnt;
@@ -339,15 +409,23 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP],
     auto issue = [&]() __attribute__((always_inline)) {
       if (o + 1 < DT) dma_image(nb, Wt + (size_t)(o + 1) * TU, TU, kC2Waves, pp.wave, pp.lane);
       else if (nextW) dma_image(nb, nextW, next_n16, kC2Waves, pp.wave, pp.lane);
-      if (o + 2 < DT) dma16(rh, slots + ((o + 2) & 3) * 64, voff, 64 * (o + 2));
-      else if (has_next_h) dma16(rh_next, slots + ((o + 2) & 3) * 64, voff, 64 * (o + 2 - DT));
+      if constexpr (B16) {
+        const int m = (o + 2) >> 1;
+        if ((o & 1) == 0) {
+          if (o + 2 < DT) dma16(rh, slots + (m & 3) * 64, voff + 16 * g, 64 * m);
+          else if (has_next_h) dma16(rh_next, slots + (m & 3) * 64, voff + 16 * g, 64 * (m - DT / 2));
+        }
+      } else {
+        if (o + 2 < DT) dma16(rh, slots + ((o + 2) & 3) * 64, voff, 64 * (o + 2));
+        else if (has_next_h) dma16(rh_next, slots + ((o + 2) & 3) * 64, voff, 64 * (o + 2 - DT));
+      }
       if (o >= 2) stores(o - 2);
     };
     f32x4 acc;
     if (o > 0) {
       // the saved h tile of the epilogue below, read now so its LDS latency hides behind the first
       // k-blocks' MFMAs (its DMA, three tiles back, was retired by the counted wait above)
-      hc = lds_read16_issue(slots + ((o - 1) & 3) * 64 + pp.lane);
+      read_h(o - 1);
       const f32x4 pv = prev;
       auto ep = [&](int r) { epi_part(o - 1, pv, r); };
 #if GNOT_C2B_PRE
@@ -364,7 +442,7 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP],
     __builtin_amdgcn_sched_barrier(0);      // no code motion across tiles (register pressure)
   }
   stores(DT - 2);
-  hc = lds_read16_issue(slots + ((DT - 1) & 3) * 64 + pp.lane);
+  read_h(DT - 1);
 #pragma unroll
   for (int r = 0; r < 4; ++r) epi_part(DT - 1, prev, r);
   stores(DT - 1);
@@ -372,7 +450,8 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP],
 
 // WALK (CH_MOE only): experts 0 .. E-1 of the workgroup's points in order; dX = sum_e W_e0^T dz_e0 summed
 // in place (expert e > 0 reads back the partial this lane stored for e-1), no stage, no combine pass.
-template <int D, int KT0, int OTL, int NP, bool WALK>
+// B16 (bf16 mode, ChainArgs::b16s): saves and dz as bf16 pair-interleaved rows
+template <int D, int KT0, int OTL, int NP, bool WALK, bool B16 = false>
 __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) {
   constexpr int DT = D / 16, KB = DT / 2, KBL = (OTL + 1) / 2;
   using LD = C2Lds<D, NP>;
@@ -385,6 +464,10 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) 
   // byte offset of this lane's row in a [P, D] layer: unsigned (the plan bounds P * D * 4 < 2^32)
   const int voff = (int)(((unsigned)(blockIdx.x * kC2Waves + wave) * 16u + (unsigned)(lane & 15)) * (unsigned)(D * 4) +
                          16u * (unsigned)g);
+  // B16: this lane's row in the bf16 layers (512 B per point)
+  const int rowb = (int)(((unsigned)(blockIdx.x * kC2Waves + wave) * 16u + (unsigned)(lane & 15)) * (unsigned)kB16Row);
+  const unsigned lay_b16 = (unsigned)min((long)a.P * kB16Row, 0xFFFFFFFFL);
+  const int lvoff = B16 ? rowb : voff;               // what the layers address rows with
   C2Pipe pp{c2lds, LD::WB, 0, wave, lane};
   constexpr int e_begin = 0;
   auto expert = [&](int e) __attribute__((always_inline)) {
@@ -396,15 +479,20 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) 
     pp.cnt = 0;
   }
   auto wt = [&](int l) { return reinterpret_cast<const u32x4*>(L[l].WpT); };
-  auto rh = [&](int l) { return make_rsrc(save + l * a.save_layer_stride, lay_bytes); };   // h_l
-  auto rz = [&](int l) { return make_rsrc(dz + l * a.dz_layer_stride, lay_bytes); };      // dz_l
-  // prologue DMA: the last Linear's tile-0 weights and the first two h_{nl-2} tiles
+  const unsigned lb = B16 ? lay_b16 : lay_bytes;
+  auto rh = [&](int l) { return make_rsrc(save + l * a.save_layer_stride, lb); };   // h_l
+  auto rz = [&](int l) { return make_rsrc(dz + l * a.dz_layer_stride, lb); };      // dz_l
+  // prologue DMA: the last Linear's tile-0 weights and the first two h_{nl-2} tiles (B16: pair 0)
   dma_image(c2lds, wt(nl - 1), c2_tile_u4(KBL, NP), kC2Waves, wave, lane);
   {
     u32x4* slots = c2lds + LD::kHs + wave * 4 * 64;
     const rsrc_t r = rh(nl - 2);
-    dma16(r, slots, voff, 0);
-    dma16(r, slots + 64, voff, 64);
+    if constexpr (B16) {
+      dma16(r, slots, rowb + 16 * g, 0);
+    } else {
+      dma16(r, slots, voff, 0);
+      dma16(r, slots + 64, voff, 64);
+    }
   }
   // ---- gradient at the chain output
   float dy[OTL][4];
@@ -412,7 +500,8 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) 
     // query_out = query_in + sum_e s_e * y_e : dy_e = s_e * dq ; ds_e = dq . y_e (model.py:128-131)
     float yv[OTL][4];
     load_rows<OTL>(dy, a.dY, a.lddy, p, valid, 16 * OTL, lane);
-    load_rows<OTL>(yv, save + (nl - 1) * a.save_layer_stride, D, p, valid, 16 * OTL, lane);
+    if constexpr (B16) load_rows_b16<OTL>(yv, rh(nl - 1), rowb, lane);
+    else load_rows<OTL>(yv, save + (nl - 1) * a.save_layer_stride, D, p, valid, 16 * OTL, lane);
     float ds = 0.f;
 #pragma unroll
     for (int T = 0; T < OTL; ++T)
@@ -445,7 +534,8 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) 
   } else {
     load_rows<OTL>(dy, a.dY, a.lddy, p, valid, a.out_dim, lane);
   }
-  store_rows<OTL>(dy, dz + (nl - 1) * a.dz_layer_stride, D, p, valid, 16 * OTL, lane);
+  if constexpr (B16) store_rows_b16<OTL>(dy, rz(nl - 1), rowb, lane);
+  else store_rows<OTL>(dy, dz + (nl - 1) * a.dz_layer_stride, D, p, valid, 16 * OTL, lane);
 
   float nx[DT][4];
   u32x4 bp[KB][NP];
@@ -455,15 +545,15 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) 
     u32x4 bl[KBL][NP];
     c2_split<OTL, NP>(dy, bl);
     const int l = nl - 1;
-    c2b_layer<KBL, NP>(pp, wt(l), bl, rh(l - 1), rz(l - 1), rh(l >= 2 ? l - 2 : 0), l - 1 >= 1, voff, next_img(l),
-                       c2_tile_u4(KB, NP), 0, nx);
+    c2b_layer<KBL, NP, B16>(pp, wt(l), bl, rh(l - 1), rz(l - 1), rh(l >= 2 ? l - 2 : 0), l - 1 >= 1, lvoff,
+                            next_img(l), c2_tile_u4(KB, NP), 0, nx);
   }
   for (int l = nl - 2; l >= 1; --l) {
     c2_split<DT, NP>(nx, bp);
-    // first wait: after the previous layer's last weight DMA, its h DMA and the stores of its last
-    // three tiles
-    c2b_layer<KB, NP>(pp, wt(l), bp, rh(l - 1), rz(l - 1), rh(l >= 2 ? l - 2 : 0), l - 1 >= 1, voff, next_img(l),
-                      c2_tile_u4(KB, NP), 1 + 3 * S_BWD, nx);
+    // first wait: after the previous layer's last weight DMA, its h DMA (B16: none at the odd last
+    // tile) and the stores of its last three tiles
+    c2b_layer<KB, NP, B16>(pp, wt(l), bp, rh(l - 1), rz(l - 1), rh(l >= 2 ? l - 2 : 0), l - 1 >= 1, lvoff,
+                           next_img(l), c2_tile_u4(KB, NP), (B16 ? 0 : 1) + 3 * S_BWD, nx);
   }
   // ---- first Linear: dX = W_0^T dz_0 (KT0 output tiles); first wait: the stores of the last layer's
   // last three tiles
@@ -519,6 +609,28 @@ static hipError_t launch_chain2_d(const ChainArgs& a, bool bwd, hipStream_t s) {
       attr = true;                                                                                       \
     }                                                                                                    \
   } while (0)
+  if (a.b16s) {
+    // bf16 storage: soft-MoE experts (d x d chains) in bf16 mode, training (saves) only
+    if constexpr (NP == 1) {
+      if (a.mode != CH_MOE || a.KT0 != DT || a.OTL != DT || (!bwd && !a.save)) return hipErrorInvalidValue;
+#define GNOT_C2_B16(W_)                                                                                  \
+  if (bwd) {                                                                                             \
+    GNOT_C2_ATTR((chain2_bwd_kernel<D, DT, DT, 1, W_, true>));                                           \
+    hipLaunchKernelGGL((chain2_bwd_kernel<D, DT, DT, 1, W_, true>), grid, block, lds, s, a);             \
+  } else {                                                                                               \
+    GNOT_C2_ATTR((chain2_fwd_kernel<D, DT, DT, true, 1, W_, true>));                                     \
+    hipLaunchKernelGGL((chain2_fwd_kernel<D, DT, DT, true, 1, W_, true>), grid, block, lds, s, a);       \
+  }
+      if (a.walk) {
+        GNOT_C2_B16(true)
+      } else {
+        GNOT_C2_B16(false)
+      }
+#undef GNOT_C2_B16
+      return hipGetLastError();
+    }
+    return hipErrorInvalidValue;
+  }
   if (a.walk) {
     // the walk form exists for the soft-MoE experts (d x d chains) only
     if (a.mode != CH_MOE || a.KT0 != DT || a.OTL != DT) return hipErrorInvalidValue;

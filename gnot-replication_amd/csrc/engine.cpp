@@ -66,6 +66,7 @@ struct WgradGroup {
   size_t slab_floats = 0;
   bool x6 = false;                   // plain weight-gradient jobs: the bf16x6 MFMA kernel
   bool wide = false;                 // ... on the 256 x 256-tile kernel (d = 256: one workgroup per job split)
+  bool b16 = false;                  // bf16-storage jobs (bf16 mode soft-MoE): pgemm_b16_kernel, wide geometry
   int state_pts = 0, state_nw = 0;
   bool state_mfma = false;   // state groups: points per workgroup, per-point weights (0 or H)
   WgradJob* d_jobs = nullptr;        // device copies (workspace tables)
@@ -186,9 +187,18 @@ struct gnot_plan {
   // soft-MoE calls in the walk form (chain2.hip: one workgroup sums all experts in place, no [P, E, d]
   // stage): decided per batch in gnot_plan_set_batch (chain2_walk_choice)
   bool moe_walk = false;
+  // input gradients (gnot_plan_set_input_grads): the x / gating / input-function encoders' first Linears
+  // also run their backward-data into dxin / dxg / dfnin<i>
+  bool input_grads = false;
   // operand pieces of the d = 256 bf16-MFMA kernels (chain2, linear2, wide weight gradients):
   // 3 = bf16x6 (fp32-exact, default), 1 = bf16 arithmetic mode (gnot_plan_set_precision)
   int np = 3;
+  // bf16 mode stores the soft-MoE chains' saves and dZ as bf16 (ChainArgs::b16s): one [P, 256] bf16 layer
+  // is P * D / 2 four-byte units, a chain's 2 * NL save slots take what NL fp32 layers did
+  bool b16s() const {
+    static const bool off = std::getenv("GNOT_NO_B16S") != nullptr;   // A/B: bf16 mode with fp32 storage
+    return np == 1 && D == 256 && !off;
+  }
   std::string msave(int l, bool m1) const {
     return moe_recompute ? std::string("mrsave") : "b" + std::to_string(l) + (m1 ? ".m1save" : ".m2save");
   }
@@ -537,6 +547,7 @@ static void finish_group(gnot_plan* p, WgradGroup& G) {
   G.wide = G.x6 && !no_wide && p->D == 256 && !G.jobs.empty();
   for (const auto& J : G.jobs)
     if (J.out > 256 || J.in > 256) G.wide = false;
+  if (G.b16) G.wide = true;          // the bf16-storage kernel has the wide kernel's geometry
   const long target = G.wide ? wide_wgs : G.x6 ? x6_wgs : kTargetWGs;
   long tiles = 0;
   for (auto& J : G.jobs) {
@@ -660,6 +671,19 @@ static void build_groups(gnot_plan* p) {
       }
     finish_group(p, G);
   };
+  // bf16-storage soft-MoE group (bf16 mode): dZ_j of chain c at dz + (c NL + j) lay, the input of Linear
+  // j > 0 in save slot NL + j of chain c, Linear 0's (the shared MoE input) in chain 0's slot NL
+  auto moe_group_b16 = [&](WgradGroup& G, int kcall, const std::vector<int>& firsts, const float* save) {
+    const float* dz = p->P_(p->dz_name(kcall));
+    const long lay = P * D / 2;
+    for (size_t c = 0; c < firsts.size(); ++c)
+      for (int j = 0; j < NL; ++j) {
+        const float* x = j == 0 ? save + NL * lay : save + ((long)c * 2 * NL + NL + j) * lay;
+        lin_job(G, firsts[c] + j, dz + ((long)c * NL + j) * lay, D, x, D, 0, P);
+      }
+    G.b16 = true;
+    finish_group(p, G);
+  };
   auto state_group = [&](WgradGroup& G, const float* A, long lda, const float* Bm, long ldb, const float* w,
                          long ldw, const std::vector<long>& off, float* state) {
     for (int b = 0; b < p->B; ++b) {
@@ -746,8 +770,13 @@ static void build_groups(gnot_plan* p) {
     const std::string s = "b" + std::to_string(l) + ".";
     std::vector<int> f1, f2;
     for (int e = 0; e < E; ++e) { f1.push_back(p->lin_f1(l, e, 0)); f2.push_back(p->lin_f2(l, e, 0)); }
-    chain_group(p->wg_m1[l], p->k_m1(l), f1, P, p->P_(s + "a"), D, p->P_(p->msave(l, true)));
-    chain_group(p->wg_m2[l], p->k_m2(l), f2, P, p->P_(s + "bb"), D, p->P_(p->msave(l, false)));
+    if (p->b16s()) {
+      moe_group_b16(p->wg_m1[l], p->k_m1(l), f1, p->P_(p->msave(l, true)));
+      moe_group_b16(p->wg_m2[l], p->k_m2(l), f2, p->P_(p->msave(l, false)));
+    } else {
+      chain_group(p->wg_m1[l], p->k_m1(l), f1, P, p->P_(s + "a"), D, p->P_(p->msave(l, true)));
+      chain_group(p->wg_m2[l], p->k_m2(l), f2, P, p->P_(s + "bb"), D, p->P_(p->msave(l, false)));
+    }
     {
       float* dsum = p->P_(p->dsum_buf(false));
       float* dqkv = p->P_(p->dqkv_buf(false));
@@ -971,6 +1000,16 @@ extern "C" int gnot_plan_set_moe_recompute(gnot_plan* p, int on) {
   return GNOT_OK;
 }
 
+extern "C" int gnot_plan_set_input_grads(gnot_plan* p, int on) {
+  if (!p) return fail(GNOT_E_INVALID, "null plan");
+  if (p->input_grads != (on != 0)) {
+    p->input_grads = on != 0;
+    p->batch_set = false;          // the workspace layout changes: set_batch + bind again
+    p->ws_bound = false;
+  }
+  return GNOT_OK;
+}
+
 extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, const int64_t* fn_off,
                                    int training) {
   if (!p || B <= 0 || !x_off) return fail(GNOT_E_INVALID, "bad batch arguments");
@@ -1005,6 +1044,8 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
   }
   p->training = training != 0;
   p->sharded = p->world > 1;
+  if (p->input_grads && p->sharded)
+    return fail(GNOT_E_INVALID, "input gradients are not available with point sharding (gnot_plan_set_input_grads)");
   if (p->sharded) {
     if ((int)p->nglob.size() != B) return fail(GNOT_E_INVALID, "gnot_plan_set_shard was declared for another B");
     for (int b = 0; b < B; ++b) {
@@ -1114,6 +1155,11 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
       }
     for (int i = 0; i < I; ++i) {
       C.add("dfn" + std::to_string(i), p->Q[i] * D, D);
+    }
+    if (p->input_grads) {
+      C.add("dxin", P * r4(p->in + p->th), r4(p->in + p->th));
+      C.add("dxg", P * r4(p->in), r4(p->in));
+      for (int i = 0; i < I; ++i) C.add("dfnin" + std::to_string(i), p->Q[i] * r4(p->F), r4(p->F));
     }
     C.add("dz0", E * NL * std::max(P, Qmax) * D, D);
     C.add("dz1", E * NL * P * D, D);
@@ -1457,6 +1503,23 @@ int guard_write(Ctx& c, const float* buf) {
   return GNOT_OK;
 }
 
+#define GNOT_RUN(expr)              \
+  do {                              \
+    const int rc_ = (expr);         \
+    if (rc_ != GNOT_OK) return rc_; \
+  } while (0)
+
+// one weight-gradient group's launches (point-reduction GEMM + split-K reduce)
+int launch_group(gnot_plan* p, const WgradGroup& G, float* slab, hipStream_t s) {
+  if (G.b16)
+    GNOT_CK(launch_wgrad_b16(G.d_jobs, G.d_wg_prefix, (int)G.jobs.size(), G.total_wgs, G.d_red_prefix, G.total_red,
+                             slab, s));
+  else
+    GNOT_CK(launch_wgrad(G.d_jobs, G.d_wg_prefix, (int)G.jobs.size(), G.total_wgs, G.d_red_prefix, G.total_red, slab,
+                         s, G.x6, G.wide, p->np));
+  return GNOT_OK;
+}
+
 // weight gradients: forked onto the side stream (off the critical path); `reads` are the main-stream
 // buffers the group consumes, guarded until it finishes
 int run_wgrad_side(Ctx& c, const WgradGroup& G, std::initializer_list<const float*> reads) {
@@ -1477,8 +1540,7 @@ int run_wgrad_side(Ctx& c, const WgradGroup& G, std::initializer_list<const floa
   if (serial || c.s == p->side2) {
     float* slab = c.s == p->side2 ? p->P_("slab_wgrad2") : p->P_("slab_wgrad");
     ProfScope ps(c, "wgrad", group_flops(G));
-    GNOT_CK(launch_wgrad(G.d_jobs, G.d_wg_prefix, (int)G.jobs.size(), G.total_wgs, G.d_red_prefix,
-                         G.total_red, slab, c.s, G.x6, G.wide, p->np));
+    GNOT_RUN(launch_group(c.p, G, slab, c.s));
     return GNOT_OK;
   }
   hipEvent_t fork = next_event(p);
@@ -1486,8 +1548,7 @@ int run_wgrad_side(Ctx& c, const WgradGroup& G, std::initializer_list<const floa
   GNOT_CK(hipStreamWaitEvent(p->side, fork, 0));
   {
     ProfScope ps(c, "wgrad", group_flops(G), p->side);
-    GNOT_CK(launch_wgrad(G.d_jobs, G.d_wg_prefix, (int)G.jobs.size(), G.total_wgs, G.d_red_prefix,
-                         G.total_red, p->P_("slab_wgrad"), p->side, G.x6, G.wide, p->np));
+    GNOT_RUN(launch_group(p, G, p->P_("slab_wgrad"), p->side));
   }
   hipEvent_t done = next_event(p);
   GNOT_CK(hipEventRecord(done, p->side));
@@ -1525,11 +1586,6 @@ int shard_exchange(Ctx& c, float* hm, float* tok, bool reverse) {
   return GNOT_OK;
 }
 
-#define GNOT_RUN(expr)              \
-  do {                              \
-    const int rc_ = (expr);         \
-    if (rc_ != GNOT_OK) return rc_; \
-  } while (0)
 
 // one LinearAttention call (model.py:53-107). q_in: the query rows [P, D].
 int attn_forward(Ctx& c, int l, bool cross, const float* q_in, float* res_out, float* out) {
@@ -1630,6 +1686,14 @@ int attn_backward(Ctx& c, int l, bool cross) {
 
 // the soft-MoE experts of one call: walk form (d = 256, chain2.hip) or the expert grid + moe_combine
 static bool moe_walk(gnot_plan* p) { return p->moe_walk; }
+// save (and dZ) layout of a soft-MoE chain call: fp32 [NL][P][D] per expert, or in bf16 mode 2 NL bf16
+// layers per expert (ChainArgs::b16s)
+static void moe_save_strides(gnot_plan* p, ChainArgs& a) {
+  const long P = p->P, D = p->D, NL = p->NL;
+  a.b16s = p->b16s() ? 1 : 0;
+  a.save_layer_stride = a.b16s ? P * D / 2 : P * D;
+  a.save_chain_stride = NL * P * D;
+}
 
 static int moe_forward(Ctx& c, const ChainTable& T, const float* in, const float* qin, float* qout, float* save) {
   gnot_plan* p = c.p;
@@ -1639,7 +1703,7 @@ static int moe_forward(Ctx& c, const ChainTable& T, const float* in, const float
   ChainArgs a = chain_args(p, T, P);
   a.X = in; a.ldx = D; a.ldy = D;
   a.scores = p->P_("scores"); a.ldsc = (int)p->bufs["scores"].ld; a.mode = CH_MOE;
-  if (save) { a.save = save; a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D; }
+  if (save) { a.save = save; moe_save_strides(p, a); }
   if (walk) {
     a.walk = 1; a.Y = qout; a.base = qin;
   } else {
@@ -1765,6 +1829,7 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
     float* dz = p->P_(p->dz_name(kcall));
     GNOT_RUN(guard_write(cc, dz));
     a.dz = dz; a.dz_layer_stride = rows * D; a.dz_chain_stride = NL * rows * D;
+    if (a.b16s) { a.dz_layer_stride /= 2; a.dz_chain_stride /= 2; }   // bf16 dZ layers
     {
       ProfScope ps(cc, prof, 2.0 * a.nchains * rows * NL * (double)D * D);
       GNOT_CK(launch_chain_bwd(a, cc.s));
@@ -1803,7 +1868,7 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
         ChainArgs f = chain_args(p, m1 ? p->ch_m1[l] : p->ch_m2[l], P);
         f.X = p->P_(s + (m1 ? "a" : "bb")); f.ldx = D; f.ldy = D;
         f.scores = p->P_("scores"); f.ldsc = (int)p->bufs["scores"].ld; f.mode = CH_MOE;
-        f.save = mr; f.save_layer_stride = P * D; f.save_chain_stride = NL * P * D;
+        f.save = mr; moe_save_strides(p, f);
         // only the saves are needed: the walk form writes no output (Y = null), the expert grid its stage
         f.walk = walk ? 1 : 0;
         f.Y = walk ? nullptr : stage; f.y_chain_stride = P * D;
@@ -1813,7 +1878,7 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
       ChainArgs a = chain_args(p, m1 ? p->ch_m1[l] : p->ch_m2[l], P);
       a.dY = dquery; a.lddy = D; a.mode = CH_MOE;
       a.scores = p->P_("scores"); a.ldsc = (int)p->bufs["scores"].ld; a.dscore = p->P_("dscore");
-      a.save = p->P_(p->msave(l, m1)); a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D;
+      a.save = p->P_(p->msave(l, m1)); moe_save_strides(p, a);
       float* dsum = p->P_(p->dsum_buf(m1));
       if (walk) {
         // d(MoE input) = sum_e W_e0^T dz_e0 summed in place by the walk form (no stage, no combine)
@@ -1863,6 +1928,7 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
     ChainArgs a = chain_args(p, p->ch_fn[i], p->Q[i]);
     a.dY = p->P_("dfn" + si); a.lddy = D; a.mode = CH_STORE;
     a.save = p->P_("fn_save" + si); a.save_layer_stride = p->Q[i] * D; a.save_chain_stride = NL * p->Q[i] * D;
+    if (p->input_grads) { a.dX = p->P_("dfnin" + si); a.lddx = p->bufs["dfnin" + si].ld; a.dx_chain_stride = 0; }
     GNOT_RUN(chain_bwd_on(cf, a, p->k_fn(i), p->Q[i], p->wg_fn[i], "chain_bwd"));
   }
   // query encoder
@@ -1870,6 +1936,7 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
     ChainArgs a = chain_args(p, p->ch_x, P);
     a.dY = dquery; a.lddy = D; a.mode = CH_STORE;
     a.save = p->P_("x_save"); a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D;
+    if (p->input_grads) { a.dX = p->P_("dxin"); a.lddx = p->bufs["dxin"].ld; a.dx_chain_stride = 0; }
     GNOT_RUN(chain_bwd(a, p->k_x(), P, p->wg_x, "chain_bwd"));
   }
   // gating: d scores accumulated over every MoE above -> softmax backward -> chain
@@ -1878,6 +1945,7 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
     a.mode = CH_SOFTMAX; a.scores = p->P_("scores"); a.ldsc = (int)p->bufs["scores"].ld;
     a.dscore = p->P_("dscore");
     a.save = p->P_("gate_save"); a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D;
+    if (p->input_grads) { a.dX = p->P_("dxg"); a.lddx = p->bufs["dxg"].ld; a.dx_chain_stride = 0; }
     GNOT_RUN(chain_bwd(a, p->k_gate(), P, p->wg_gate, "chain_bwd"));
   }
   if (br) {                                // join the input-function branch
@@ -1890,6 +1958,23 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
   GNOT_CK(hipEventRecord(join, p->side));
   GNOT_CK(hipStreamWaitEvent(c.s, join, 0));
   p->readers.clear();
+  return GNOT_OK;
+}
+
+// reference autograd's gradients of x, theta and the input functions (model.py:155-166), from the
+// encoders' input gradients of the last gnot_backward
+extern "C" int gnot_input_grads(gnot_plan* p, float* dx, float* dtheta, float* const* dfns, void* stream) {
+  if (!p || !p->input_grads || !p->ws_bound || !p->training)
+    return fail(GNOT_E_STATE, "gnot_plan_set_input_grads(plan, 1) and a training batch are required");
+  const hipStream_t s = static_cast<hipStream_t>(stream);
+  const Buf& xin = p->bufs.at("dxin");
+  const Buf& xg = p->bufs.at("dxg");
+  if (dx) GNOT_CK(launch_add_cols(xin.p, xin.ld, xg.p, xg.ld, p->in, dx, p->P, s));
+  if (dtheta) GNOT_CK(launch_seg_colsum(xin.p, xin.ld, p->in, p->th, p->d_xoff, p->B, dtheta, s));
+  for (int i = 0; dfns && i < p->I; ++i) {
+    const Buf& f = p->bufs.at("dfnin" + std::to_string(i));
+    if (dfns[i]) GNOT_CK(launch_add_cols(f.p, f.ld, nullptr, 0, p->F, dfns[i], p->Q[i], s));
+  }
   return GNOT_OK;
 }
 

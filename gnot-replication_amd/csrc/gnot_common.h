@@ -65,6 +65,15 @@ GNOT_DEV float gelu(float x) {
   asm("v_max_f32 %0, 0, %1" : "=v"(r) : "v"(x));
   return fmaf(-fabsf(x), q, r);
 }
+// gelu(x) (bitwise as gelu()) and gelu'(x) from one tail evaluation
+GNOT_DEV float gelu_and_grad(float x, float& dg) {
+  float e;
+  const float q = gelu_tail(x, e);
+  float r;
+  asm("v_max_f32 %0, 0, %1" : "=v"(r) : "v"(x));
+  dg = fmaf(x * kInvSqrt2Pi, e, 0.5f + copysignf(0.5f - q, x));
+  return fmaf(-fabsf(x), q, r);
+}
 GNOT_DEV float gelu_grad(float x) {
   float e;
   const float q = gelu_tail(x, e);
@@ -389,6 +398,56 @@ GNOT_DEV void split2_np(float v0, float v1, u32x4 (&p)[NP], int d) {
   } else {
     p[0][d] = (bf16_rne_bits(v1) << 16) | bf16_rne_bits(v0);
   }
+}
+
+// ---- bf16 activation rows (bf16 arithmetic mode, soft-MoE chains at d = 256) ---------------------
+// "Pair-interleaved" (PI) rows of 256 bf16 = 512 B per point: feature f = 16T + 4g + r sits in 16-byte
+// chunk (T >> 1) * 4 + g, 8-byte half T & 1, element r.  Chunk (t, g) of a point is exactly the word a
+// point-form lane of group g packs for k-block t (split_block_x6: tiles 2t, 2t+1), so the chains load and
+// store whole 16-byte operand words, and every 4 consecutive features (f % 4 == 0) are 8 contiguous
+// bytes: the row pieces ds_read_b64_tr_b16 gathers in the weight-gradient kernel (wgrad.hip).
+constexpr int kB16Row = 512;
+GNOT_DEV int b16_off(int T, int g) { return ((T >> 1) * 4 + g) * 16 + (T & 1) * 8; }
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+// RNE bf16 of two floats in one word (v_cvt_pk_bf16_f32: the bits of bf16_rne_bits for finite values)
+GNOT_DEV unsigned pk_bf16(float lo, float hi) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  const bf16x2 v = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(unsigned, v);
+}
+GNOT_DEV float bf16_lo(unsigned w) { return u2f(w << 16); }
+GNOT_DEV float bf16_hi(unsigned w) { return u2f(w & 0xFFFF0000u); }
+// 8-byte buffer store (whole offset in the VGPR, soffset 0: see buf_store_f32x4)
+GNOT_DEV void buf_store_b64(u32x2 v, rsrc_t r, int voff) { __builtin_amdgcn_raw_buffer_store_b64(v, r, voff, 0, 0); }
+GNOT_DEV void buf_store_b128(u32x4 v, rsrc_t r, int voff) { __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, 0, 0); }
+// one point-form tile (4 features of this lane) as RNE bf16 at its PI position; rowoff = point * 512
+GNOT_DEV void store_tile_b16(const float (&v)[4], rsrc_t r, int rowoff, int T, int g) {
+  buf_store_b64(u32x2{pk_bf16(v[0], v[1]), pk_bf16(v[2], v[3])}, r, rowoff + b16_off(T, g));
+}
+// KT point-form tiles from / to PI bf16 rows (KT even; rows past the resource bound read 0 / are dropped)
+template <int KT>
+GNOT_DEV void load_rows_b16(float (&a)[KT][4], rsrc_t r, int rowoff, int lane) {
+  const int g = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < KT / 2; ++t) {
+    const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(r, rowoff + (t * 4 + g) * 16, 0, 0);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      a[2 * t + h][0] = bf16_lo(w[2 * h]);
+      a[2 * t + h][1] = bf16_hi(w[2 * h]);
+      a[2 * t + h][2] = bf16_lo(w[2 * h + 1]);
+      a[2 * t + h][3] = bf16_hi(w[2 * h + 1]);
+    }
+  }
+}
+template <int KT>
+GNOT_DEV void store_rows_b16(const float (&a)[KT][4], rsrc_t r, int rowoff, int lane) {
+  const int g = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < KT / 2; ++t)
+    buf_store_b128(u32x4{pk_bf16(a[2 * t][0], a[2 * t][1]), pk_bf16(a[2 * t][2], a[2 * t][3]),
+                         pk_bf16(a[2 * t + 1][0], a[2 * t + 1][1]), pk_bf16(a[2 * t + 1][2], a[2 * t + 1][3])},
+                   r, rowoff + (t * 4 + g) * 16);
 }
 
 // B pieces of k-block t of the point-form activations in[KT][4]: bp[q] = 8 bf16 (4 dwords) of piece q

@@ -92,6 +92,14 @@ struct ChainArgs {
   // be null (MoE recompute: saves only).
   int walk = 0;
   const float* base = nullptr;       // walk forward: the residual (query in); null = 0
+  // CH_MOE, d = 256, np = 1 (bf16 mode): bf16 activation storage.  Saves and dZ are bf16 "pair-
+  // interleaved" rows (gnot_common.h, 512 B per point; strides above then count 4-byte units, so a
+  // [P, 256] bf16 layer is P * 128 of them).  Per chain, save slots 0 .. nlin-2 hold gelu'(h_l) of the
+  // GELU layers (the backward's factor, computed with gelu(h_l) in the forward), slot nlin-1 the expert
+  // output y (read back for d score), slots nlin + l the RNE bf16 input of Linear l (= gelu(h_{l-1}), the
+  // MFMA operand the forward used), written for the weight gradients; slot nlin + 0 (the shared MoE
+  // input) only in chain 0.
+  int b16s = 0;
 };
 // walk or per-expert grid for a MoE call of P points (env GNOT_MOE_WALK = 0 / 1 forces, read per call)
 bool chain2_walk_choice(long P, int E);
@@ -127,6 +135,10 @@ struct WgradJob {
 hipError_t launch_wgrad(const WgradJob* jobs_dev, const int* wg_prefix_dev, int njobs, int total_wgs,
                         const int* red_prefix_dev, int total_red, float* slab, hipStream_t s, bool x6 = false,
                         bool wide = false, int np = 3);   // np: the wide kernel's operand pieces (1 = bf16 mode)
+// bf16-storage jobs (ChainArgs::b16s): dz and x point at bf16 pair-interleaved rows [P, 256] (x already
+// the Linear's input, no GELU), out = in = 256, one workgroup per (job, split) as the wide kernel
+hipError_t launch_wgrad_b16(const WgradJob* jobs_dev, const int* wg_prefix_dev, int njobs, int total_wgs,
+                            const int* red_prefix_dev, int total_red, float* slab, hipStream_t s);
 
 // ------------------------------------------------------------------ attention states (state.hip)
 // Jobs are WgradJobs with state_dh > 0: A = dz/lddz, B = x/ldx, optional w/ldw, out = dW as
@@ -195,6 +207,12 @@ hipError_t launch_concat_theta(const float* x, long ldx, int in_dim, const float
 // out = (base ? base : 0) + sum_e stage[e]
 hipError_t launch_moe_combine(const float* base, const float* stage, long stage_stride, int E,
                               float* out, long n, hipStream_t s);
+// out[r][c] = a[r][c] + b[r][c] (b null: a copy), c < cols, out dense [rows, cols]
+hipError_t launch_add_cols(const float* a, long lda, const float* b, long ldb, int cols, float* out, long rows,
+                           hipStream_t s);
+// out[b][t] = sum over rows [off[b], off[b+1]) of a[row][c0 + t], t < ncols (fixed order)
+hipError_t launch_seg_colsum(const float* a, long lda, int c0, int ncols, const long* off, int B, float* out,
+                             hipStream_t s);
 // segmented copy: dst[seg.dst + i] = src[seg.src + i], i < seg.len (floats, multiples of 4);
 // reverse swaps the roles of src/dst offsets.  prefix4: float4 prefix sums of the lengths [nseg + 1].
 struct CopySeg {

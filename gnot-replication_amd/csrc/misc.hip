@@ -5,6 +5,9 @@
 //                  (q_in may be null: plain sum, used for the expert-summed dX of the MoE backward)
 //   segcopy      : table-driven float4 copy of contiguous runs (the point-shard scramble all-to-all's
 //                  pack / unpack, engine.cpp build_exchange)
+//   input grads  : d x = d x_in[:, :in] + d x_gate (x feeds the encoder through cat and the gating MLP,
+//                  model.py:155, 158-161), d theta[b] = sum over sample b's points of d x_in[:, in:]
+//                  (the broadcast of model.py:158), d fn = the encoder chain's input gradient
 #include "gnot_common.h"
 #include "gnot_kernels.h"
 
@@ -89,6 +92,49 @@ hipError_t launch_segcopy(const CopySeg* segs, const int* prefix4, int nseg, int
   const int blocks = std::min((total4 + 255) / 256, 4096);
   hipLaunchKernelGGL(segcopy_kernel, dim3(blocks), dim3(256), 0, s, segs, prefix4, nseg, total4, src, dst,
                      reverse ? 1 : 0);
+  return hipGetLastError();
+}
+
+// d x [P, in] = a[:, :in] + b[:, :in] (b may be null); a plain column copy when b is null
+__global__ void __launch_bounds__(256) add_cols_kernel(const float* __restrict__ a, long lda, const float* __restrict__ b,
+                                                       long ldb, int cols, float* __restrict__ out, long rows) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * cols) return;
+  const long r = i / cols;
+  const int c = (int)(i % cols);
+  out[i] = b ? a[r * lda + c] + b[r * ldb + c] : a[r * lda + c];
+}
+
+// d theta[b][t] = sum_{p in sample b} a[p][c0 + t]: one workgroup per (b, t), strided partial sums then a
+// fixed-order tree in LDS (deterministic)
+__global__ void __launch_bounds__(256) seg_colsum_kernel(const float* __restrict__ a, long lda, int c0, int ncols,
+                                                         const long* __restrict__ off, float* __restrict__ out) {
+  __shared__ float red[256];
+  const int b = blockIdx.x, t = blockIdx.y;
+  float acc = 0.f;
+  for (long p = off[b] + threadIdx.x; p < off[b + 1]; p += 256) acc += a[p * lda + c0 + t];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[(long)b * ncols + t] = red[0];
+}
+
+hipError_t launch_add_cols(const float* a, long lda, const float* b, long ldb, int cols, float* out, long rows,
+                           hipStream_t s) {
+  const long n = rows * cols;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(add_cols_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a, lda, b, ldb, cols, out,
+                     rows);
+  return hipGetLastError();
+}
+
+hipError_t launch_seg_colsum(const float* a, long lda, int c0, int ncols, const long* off, int B, float* out,
+                             hipStream_t s) {
+  if (B <= 0 || ncols <= 0) return hipSuccess;
+  hipLaunchKernelGGL(seg_colsum_kernel, dim3(B, ncols), dim3(256), 0, s, a, lda, c0, ncols, off, out);
   return hipGetLastError();
 }
 

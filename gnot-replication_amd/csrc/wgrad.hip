@@ -19,6 +19,7 @@
 
 #include "gnot_common.h"
 #include "gnot_kernels.h"
+#include "x6_core.h"
 
 namespace gnot {
 
@@ -683,6 +684,145 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
   }
 }
 
+// ---------------------------------------------------------------- bf16-storage variant (bf16 mode)
+// In bf16 mode the soft-MoE chains store dZ and every Linear's input (gelu already applied, RNE bf16: the
+// operand bits the forward's MFMAs used) as pair-interleaved rows (gnot_common.h), so this kernel stages
+// nothing by hand:
+//   DMA:  32-point stages of both operands (2 x 16 KiB) land by LDS-DMA in a 4-slot ring with three
+//         stages in flight per workgroup (96 KiB: about one CU's share of HBM bandwidth x latency).  One
+//         wave-instruction brings two 512-byte rows; the lane at chunk position c of row r fetches chunk
+//         c ^ 4 (r & 3), so the 4 rows one 16-lane transposed read touches sit on disjoint banks;
+//   MFMA: ds_read_b64_tr_b16 turns the point-major rows into v_mfma_f32_32x32x16_bf16 fragments (lane i
+//         of a 16-lane group receives 4 points of feature i); wave (wr, wc) owns rows [128 wr, +128) x
+//         cols [64 wc, +64) as in the wide kernel; db (column sums of dZ) comes from the fragment of row
+//         block wc that each wave reads anyway.
+// Cost per point and job: 1 KiB of HBM against 2 x 256 x 256 flops (128 flop/B): HBM-bound.
+constexpr int kBStage = 32;
+constexpr int kBSlots = 4;
+constexpr int kBOpnd = kBStage * kB16Row;                  // bytes per operand per stage (16 KiB)
+constexpr int kBSlotBytes = 2 * kBOpnd;
+constexpr size_t kBLds = (size_t)kBSlots * kBSlotBytes;    // 128 KiB
+
+GNOT_DEV u32x2 lds_tr_b64(unsigned addr) {
+  u32x2 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(addr) : "memory");
+  return v;
+}
+
+__global__ void __launch_bounds__(kWThreads) pgemm_b16_kernel(const WgradJob* __restrict__ jobs,
+                                                             const int* __restrict__ prefix, int njobs,
+                                                             float* __restrict__ slab) {
+  extern __shared__ __attribute__((aligned(16))) u32x4 bl[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int j = find_job(prefix, njobs, blockIdx.x);
+  const WgradJob J = jobs[j];
+  const int split = blockIdx.x - prefix[j];
+  const int chunk = ((J.P + J.splits - 1) / J.splits + kBStage - 1) / kBStage * kBStage;
+  const long pb = (long)split * chunk;
+  const long pe = min((long)J.P, pb + chunk);
+  const int nst = pe > pb ? (int)((pe - pb + kBStage - 1) / kBStage) : 0;
+  const int wr = wave >> 2, wc = wave & 3;
+  // rows past the job's P read 0 (only the last split's last stage reaches past it)
+  const unsigned bytes = (unsigned)min((long)J.P * kB16Row, 0xFFFFFFFFL);
+  const rsrc_t rA = make_rsrc(J.dz, bytes), rB = make_rsrc(J.x, bytes);
+  // DMA role: wave w brings rows 2w, 2w+1 (instruction 0) and 2w+16, 2w+17 (instruction 1) of both
+  // operands; (r & 3) is the same for both instructions
+  const int hi = lane >> 5;
+  const int dvoff = hi * kB16Row + (((lane & 31) ^ (((2 * wave + hi) & 3) << 2)) * 16);
+  auto dma_stage = [&](int s) __attribute__((always_inline)) {
+    const unsigned p0 = (unsigned)(pb + (long)s * kBStage);
+    u32x4* slot = bl + (s % kBSlots) * (kBSlotBytes / 16);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = 2 * wave + 16 * i;
+      const int soff = (int)((p0 + (unsigned)row) * (unsigned)kB16Row);
+      dma16(rA, slot + row * (kB16Row / 16), dvoff, soff);
+      dma16(rB, slot + (kBOpnd + row * kB16Row) / 16, dvoff, soff);
+    }
+  };
+  // transposed-read address of feature block m (32 features = PI chunk column m), K-step ks (16 points),
+  // half h (4 points): lane 4q + pq of group G reads row 16 ks + 8 (G >> 1) + 4 h + q, features
+  // 32 m + 16 (G & 1) + 4 pq .. + 3 = chunk m * 4 + pq (position (m ^ q) * 4 + pq), half G & 1
+  const int G = lane >> 4, q = (lane >> 2) & 3, pq = lane & 3;
+  const unsigned lds0 = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) u32x4*)bl;
+  auto frag = [&](unsigned base, int m, int ks) {
+    const unsigned a = base + (unsigned)((16 * ks + 8 * (G >> 1) + q) * kB16Row + (((m ^ q) * 4 + pq) * 16) + (G & 1) * 8);
+    const u32x2 x0 = lds_tr_b64(a), x1 = lds_tr_b64(a + 4 * kB16Row);
+    return u32x4{x0[0], x0[1], x1[0], x1[1]};
+  };
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{};
+  float dbacc = 0.f;
+  for (int s = 0; s < 3 && s < nst; ++s) dma_stage(s);
+  for (int s = 0; s < nst; ++s) {
+    // stage s has landed (this wave's DMAs of stages s+1, s+2 stay in flight: 4 each) and every wave is
+    // done with stage s-1, whose slot stage s+3 refills
+    c2_sync_n(4 * min(2, nst - 1 - s));
+    if (s + 3 < nst) dma_stage(s + 3);
+    const unsigned base = lds0 + (unsigned)((s % kBSlots) * kBSlotBytes);
+    u32x4 af[2][4], bf[2][2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int ib = 0; ib < 4; ++ib) af[ks][ib] = frag(base, 4 * wr + ib, ks);
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb) bf[ks][jb] = frag(base + kBOpnd, 2 * wc + jb, ks);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      // the reads are inline asm: the compiler does not know they are pending, so wait for them by name
+      // (K-step 1's reads stay in flight under K-step 0's MFMAs)
+      __builtin_amdgcn_sched_barrier(0);
+      if (ks == 0)
+        asm volatile("s_waitcnt lgkmcnt(12)" : "+v"(af[0][0]), "+v"(af[0][1]), "+v"(af[0][2]), "+v"(af[0][3]),
+                     "+v"(bf[0][0]), "+v"(bf[0][1])::"memory");
+      else
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(af[1][0]), "+v"(af[1][1]), "+v"(af[1][2]), "+v"(af[1][3]),
+                     "+v"(bf[1][0]), "+v"(bf[1][1])::"memory");
+#pragma unroll
+      for (int ib = 0; ib < 4; ++ib)
+        if (ib == wc) {
+          const u32x4 w = af[ks][ib];
+#pragma unroll
+          for (int d = 0; d < 4; ++d) dbacc += bf16_lo(w[d]) + bf16_hi(w[d]);
+        }
+#pragma unroll
+      for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+        for (int jb = 0; jb < 2; ++jb)
+          acc[ib][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, af[ks][ib]),
+                                                                __builtin_bit_cast(bf16x8, bf[ks][jb]), acc[ib][jb], 0,
+                                                                0, 0);
+    }
+  }
+
+  // partials -> slab [split][128-tile][128 x (128 + 1)] (the pgemm_kernel layout)
+  const int ntile = J.tiles_o * J.tiles_i;
+  float* S0 = slab + J.slab_off + (long)split * ntile * (kTile * (kTile + 1));
+#pragma unroll
+  for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wr * 128 + ib * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int col = wc * 64 + jb * 32 + (lane & 31);
+        S0[((row >> 7) * J.tiles_i + (col >> 7)) * (kTile * (kTile + 1)) + (row & 127) * (kTile + 1) + (col & 127)] =
+            acc[ib][jb][r];
+      }
+  // db: lane l summed points of half l >> 5 of feature 128 wr + 32 wc + (l & 31)
+  dbacc += shfl_xor(dbacc, 32);
+  if (J.db != nullptr && lane < 32) {
+    const int f = wr * 128 + wc * 32 + lane;
+    S0[((f >> 7) * J.tiles_i) * (kTile * (kTile + 1)) + (f & 127) * (kTile + 1) + kTile] = dbacc;
+  }
+}
+
 // sum the split partials; normal jobs write dW[out, in] (+ db[out]); state jobs (state_dh > 0) write
 // the per-head diagonal blocks into [H][dh*dh + dh] (S row-major, then z)
 __global__ void __launch_bounds__(256) pgemm_reduce_kernel(const WgradJob* __restrict__ jobs,
@@ -729,6 +869,21 @@ __global__ void __launch_bounds__(256) pgemm_reduce_kernel(const WgradJob* __res
     dst = isdb ? (J.db + row) : (J.dW + (long)row * J.in + col);
   }
   *dst = J.accumulate ? (*dst + s) : s;
+}
+
+hipError_t launch_wgrad_b16(const WgradJob* jobs_dev, const int* wg_prefix_dev, int njobs, int total_wgs,
+                            const int* red_prefix_dev, int total_red, float* slab, hipStream_t s) {
+  if (njobs <= 0) return hipSuccess;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(pgemm_b16_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kBLds);
+    attr = true;
+  }
+  hipLaunchKernelGGL(pgemm_b16_kernel, dim3(total_wgs), dim3(kWThreads), kBLds, s, jobs_dev, wg_prefix_dev, njobs, slab);
+  hipLaunchKernelGGL(pgemm_reduce_kernel, dim3((total_red + 255) / 256), dim3(256), 0, s, jobs_dev, red_prefix_dev,
+                     njobs, total_red, (const float*)slab);
+  return hipGetLastError();
 }
 
 hipError_t launch_wgrad(const WgradJob* jobs_dev, const int* wg_prefix_dev, int njobs, int total_wgs,

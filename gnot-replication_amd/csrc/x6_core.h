@@ -157,6 +157,12 @@ GNOT_DEV void c2_sync_n(int n) {   // n is wave-uniform and small
     case 4: c2_sync<4>(); break;
     case 5: c2_sync<5>(); break;
     case 6: c2_sync<6>(); break;
+    case 7: c2_sync<7>(); break;
+    case 8: c2_sync<8>(); break;
+    case 9: c2_sync<9>(); break;
+    case 10: c2_sync<10>(); break;
+    case 11: c2_sync<11>(); break;
+    case 12: c2_sync<12>(); break;
     default: c2_sync<0>(); break;
   }
 }
@@ -186,6 +192,13 @@ GNOT_DEV f32x4 lds_read16_issue(const u32x4* p) {
   f32x4 v;
   const unsigned a = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) u32x4*)p;
   asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a) : "memory");
+  return v;
+}
+// 8-byte form of lds_read16_issue (bf16 saved tiles): `byte` is added to the slot address
+GNOT_DEV u32x2 lds_read8_issue(const u32x4* p, int byte) {
+  u32x2 v;
+  const unsigned a = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) u32x4*)p + (unsigned)byte;
+  asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(a) : "memory");
   return v;
 }
 // this wave's own LDS-DMA (lane l: 16 B at lds + l) from a buffer resource at byte offset voff + soff

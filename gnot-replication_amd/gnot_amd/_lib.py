@@ -25,7 +25,8 @@ class GnotConfig(ctypes.Structure):
 EXPORTS = [
     "gnot_plan_create", "gnot_plan_destroy", "gnot_plan_num_linears", "gnot_plan_linear_dims",
     "gnot_plan_bind_params", "gnot_plan_set_batch", "gnot_plan_workspace_bytes",
-    "gnot_plan_bind_workspace", "gnot_plan_bind_workspace_async", "gnot_plan_set_moe_recompute", "gnot_plan_set_precision", "gnot_plan_grad_offsets", "gnot_pack_weights", "gnot_forward",
+    "gnot_plan_bind_workspace", "gnot_plan_bind_workspace_async", "gnot_plan_set_moe_recompute", "gnot_plan_set_precision",
+    "gnot_plan_set_input_grads", "gnot_input_grads", "gnot_plan_grad_offsets", "gnot_pack_weights", "gnot_forward",
     "gnot_backward", "gnot_profile_enable", "gnot_profile_read", "gnot_debug_buffer", "gnot_last_error",
     "gnot_version", "gnot_plan_set_shard", "gnot_shard_range", "gnot_shard_exchange",
     "gnot_rel_l2_work_floats", "gnot_rel_l2_loss", "gnot_adamw_step",
@@ -66,6 +67,8 @@ def _declare(lib):
     lib.gnot_plan_bind_workspace_async.argtypes = [P, P, sz, P]
     lib.gnot_plan_set_moe_recompute.argtypes = [P, ctypes.c_int]
     lib.gnot_plan_set_precision.argtypes = [P, ctypes.c_int]
+    lib.gnot_plan_set_input_grads.argtypes = [P, ctypes.c_int]
+    lib.gnot_input_grads.argtypes = [P, P, P, ctypes.POINTER(P), P]
     lib.gnot_plan_grad_offsets.argtypes = [P, ctypes.POINTER(i64)]
     lib.gnot_pack_weights.argtypes = [P, P]
     lib.gnot_forward.argtypes = [P, P, P, ctypes.POINTER(P), P, P]

@@ -43,6 +43,7 @@ class Engine:
         self.comm = None           # parallel.PointShardComm when points are sharded over ranks
         self.moe_recompute = False # re-run each MoE call's expert forward in the backward (memory option)
         self.bf16 = False          # bf16 arithmetic mode of the d = 256 MFMA kernels (gnot_plan_set_precision)
+        self.input_grads = False   # also differentiate x, theta, input functions (gnot_plan_set_input_grads)
         self.fwd_token = 0
 
     def __del__(self):
@@ -71,7 +72,8 @@ class Engine:
         n_global: per-sample global point counts when the points are sharded over ranks (self.comm)."""
         self._bind_params()
         geom = (tuple(x_off), tuple(tuple(o) for o in fn_offs), bool(training),
-                tuple(n_global) if n_global is not None else None, bool(self.moe_recompute), bool(self.bf16))
+                tuple(n_global) if n_global is not None else None, bool(self.moe_recompute), bool(self.bf16),
+                bool(self.input_grads) and bool(training))
         if geom == self.geom:
             return
         B = len(x_off) - 1
@@ -88,6 +90,7 @@ class Engine:
             _lib.check(self.lib.gnot_plan_set_shard(self.plan, 0, 1, 0, None, None))
         _lib.check(self.lib.gnot_plan_set_moe_recompute(self.plan, int(bool(self.moe_recompute))))
         _lib.check(self.lib.gnot_plan_set_precision(self.plan, int(bool(self.bf16))))
+        _lib.check(self.lib.gnot_plan_set_input_grads(self.plan, int(bool(self.input_grads) and bool(training))))
         xo = (ctypes.c_int64 * (B + 1))(*x_off)
         flat = [v for o in fn_offs for v in o]
         fo = (ctypes.c_int64 * max(1, len(flat)))(*flat) if flat else None
@@ -157,6 +160,14 @@ class Engine:
         _lib.check(self.lib.gnot_forward(self.plan, x.data_ptr(), theta.data_ptr(), fptr, out.data_ptr(), s))
         self.fwd_token += 1
         return self.fwd_token
+
+    def input_grads_into(self, dx, dtheta, dfns):
+        """Gradients of x [P, in], theta [B, th] and the input functions [Q_i, F] of the last backward
+        (None entries are skipped); launched on torch's current stream."""
+        ptr = lambda t: t.data_ptr() if t is not None else None
+        fptr = _ptr_array([ptr(f) for f in dfns]) if dfns else None
+        with torch.cuda.device(self.ws.device):
+            _lib.check(self.lib.gnot_input_grads(self.plan, ptr(dx), ptr(dtheta), fptr, self.stream()))
 
     def backward(self, dout):
         with torch.cuda.device(self.ws.device):

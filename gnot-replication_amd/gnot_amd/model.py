@@ -82,13 +82,21 @@ class HeterogeneousNormalizedAttentionBlock(nn.Module):
 
 
 class _GNOTFunction(torch.autograd.Function):
+    """Inputs: (engine, out_dim, n_fns, x, theta, *fns, *weights, *biases).  The backward returns every
+    parameter gradient and, when the engine was prepared with input gradients (x, theta or an input
+    function requires grad, as the reference's autograd would differentiate them, model.py:154-173),
+    the gradients of x, theta and the input functions."""
+
     @staticmethod
-    def forward(ctx, engine, x, theta, fns, out_dim, *params):
+    def forward(ctx, engine, out_dim, nfn, x, theta, *rest):
+        fns = list(rest[:nfn])
         P = x.shape[0]
         out = torch.empty(P, out_dim, device=x.device, dtype=torch.float32)
         ctx.engine = engine
         ctx.token = engine.forward(x, theta, fns, out)
-        ctx.nparams = len(params)
+        ctx.nfn = nfn
+        ctx.in_shapes = (tuple(x.shape), tuple(theta.shape), [tuple(f.shape) for f in fns])
+        ctx.nparams = len(rest) - nfn
         return out
 
     @staticmethod
@@ -98,11 +106,20 @@ class _GNOTFunction(torch.autograd.Function):
             raise RuntimeError("gnot_amd keeps the activations of the most recent forward only; "
                                "backward must follow its own forward")
         eng.backward(dout.contiguous().float())
+        nfn = ctx.nfn
+        need = ctx.needs_input_grad
+        in_grads = [None] * (2 + nfn)
+        if eng.input_grads and any(need[3:5 + nfn]):
+            xs, ts, fs = ctx.in_shapes
+            new = lambda shape, want: torch.empty(shape, device=dout.device, dtype=torch.float32) if want else None
+            in_grads = [new(xs, need[3]), new(ts, need[4])] + [new(fs[i], need[5 + i]) for i in range(nfn)]
+            eng.input_grads_into(in_grads[0], in_grads[1], in_grads[2:])
+        head = (None, None, None, *in_grads)
         if not eng.param_grads:
             # the caller consumes the arena itself (gnot_amd.train.FlatAdamW) before the next backward:
             # no copy, and autograd accumulates nothing into .grad
             eng.grad_flat = eng.grad_arena
-            return (None, None, None, None, None) + (None,) * ctx.nparams
+            return head + (None,) * ctx.nparams
         # ONE copy of the whole gradient arena (the workspace is reused by the next step); every
         # parameter gradient is a view of that fresh buffer
         flat = eng.grad_arena.clone()
@@ -112,7 +129,7 @@ class _GNOTFunction(torch.autograd.Function):
             ws.append(flat[off_w:off_w + shape_w[0] * shape_w[1]].view(shape_w))
             bs.append(flat[off_b:off_b + nb])
         # params were passed as (all weights..., all biases...)
-        return (None, None, None, None, None, *ws, *bs)
+        return head + (*ws, *bs)
 
 
 class GNOT(nn.Module):
@@ -159,8 +176,10 @@ class GNOT(nn.Module):
     def set_precision(self, dtype):
         """'fp32' (default: the reference's fp32 arithmetic, bf16x6-exact on the MFMA) or 'bf16' (BASELINE
         configs[2]'s bf16 training: ONE round-to-nearest bf16 operand piece per MFMA in the d = 256 MLP
-        chains, attention projections and weight gradients, fp32 accumulation; parameters, activations
-        and the attention contractions stay fp32).  Other hidden widths are unaffected."""
+        chains, attention projections and weight gradients, fp32 accumulation; the soft-MoE expert chains
+        keep their training saves (gelu'(h), expert outputs), dZ and Linear inputs in bf16, which the MoE
+        weight gradients read directly; parameters, the other activations and the attention contractions
+        stay fp32).  Other hidden widths are unaffected."""
         d = str(dtype).replace("torch.", "")
         if d in ("bf16", "bfloat16"):
             self._bf16 = True
@@ -220,10 +239,13 @@ class GNOT(nn.Module):
         theta = theta.contiguous().float()
         fns = [f.contiguous().float() for f in fns]
         params = [l.weight for l in self.linears()] + [l.bias for l in self.linears()]
-        training = torch.is_grad_enabled() and any(p.requires_grad for p in params)
+        grad = torch.is_grad_enabled()
+        inputs_grad = grad and (x.requires_grad or theta.requires_grad or any(f.requires_grad for f in fns))
+        training = grad and (inputs_grad or any(p.requires_grad for p in params))
         eng = self.engine()
+        eng.input_grads = inputs_grad
         # every launch (and the plan's side streams) on x's device, whatever device is current
         with torch.cuda.device(x.device):
             eng.prepare([int(v) for v in x_off], [[int(v) for v in o] for o in fn_offs], training, x.device,
                         n_global=None if n_global is None else [int(n) for n in n_global])
-            return _GNOTFunction.apply(eng, x, theta, fns, self._cfg["out_dim"], *params)
+            return _GNOTFunction.apply(eng, self._cfg["out_dim"], len(fns), x, theta, *fns, *params)

@@ -89,10 +89,23 @@ int gnot_plan_set_moe_recompute(gnot_plan* plan, int on);
 /* Arithmetic mode of the d = 256 MFMA kernels (MLP chains, attention projections, weight gradients):
  * bf16 == 0 (default) runs them as bf16x6 -- three exact bf16 pieces per fp32 operand, six products,
  * fp32-level results (north_star's 1e-4 bar); bf16 != 0 runs ONE round-to-nearest-even bf16 piece per
- * operand with fp32 accumulation (BASELINE configs[2]'s bf16 training; north_star's 1e-2 bar).
- * Activations, states, gradients and the attention contractions stay fp32 either way; other widths
- * are unaffected.  Changing it invalidates the batch (set_batch + bind again). */
+ * operand with fp32 accumulation (BASELINE configs[2]'s bf16 training; north_star's 1e-2 bar), and
+ * the soft-MoE expert chains keep their training saves, dZ and Linear inputs as bf16 rows (the MoE
+ * weight gradients read them directly).  Parameters, the other activations, states, gradients and the
+ * attention contractions stay fp32 either way; other widths are unaffected.  Changing it invalidates
+ * the batch (set_batch + bind again). */
 int gnot_plan_set_precision(gnot_plan* plan, int bf16);
+
+/* Input gradients (off by default).  The reference's autograd also differentiates w.r.t. x, theta and
+ * the input functions when they require grad (model.py:154-173: x feeds the gating MLP and, through
+ * torch.cat with the broadcast theta, the query encoder; the input functions feed their encoder
+ * MLPs).  With on != 0 the backward also runs the first Linear's backward-data of those four encoders;
+ * gnot_input_grads then writes dx [P, input_dim], dtheta [B, theta_dim] (sums over each sample's
+ * points) and dfns[i] [Q_i, input_func_dim] (any pointer may be null: skipped).  Training plans only;
+ * not with point sharding (theta's gradient would be a per-rank partial sum).  Changing it invalidates
+ * the batch (set_batch + bind again). */
+int gnot_plan_set_input_grads(gnot_plan* plan, int on);
+int gnot_input_grads(gnot_plan* plan, float* dx, float* dtheta, float* const* dfns, void* stream);
 
 /* Workspace: bytes needed for the current config + batch; bind a device buffer of at least that
  * size (256-byte aligned).  Binding uploads the plan's small device tables: gnot_plan_bind_workspace

@@ -1,0 +1,135 @@
+"""Input gradients (gnot_plan_set_input_grads / gnot_input_grads through gnot_amd.GNOT's autograd).
+
+When x, theta or an input function requires grad, the reference's autograd differentiates them too
+(model.py:154-173): x feeds the gating MLP (model.py:155) and, concatenated with the per-sample
+broadcast theta, the query encoder (model.py:158-161); each input function feeds its encoder MLP
+(model.py:164-166).  The engine runs the first Linear's backward-data of those encoders and
+gnot_input_grads combines them (dx = d x_in[:, :in] + d x_gate, d theta = per-sample sums).
+
+Checked against float64 autograd of the stock-torch port (oracle/torch_port.py; its forward and
+parameter gradients are pinned to the reference's fixtures by tests/test_oracle.py, the input
+gradients are torch's autograd of that same op sequence) at north_star's 1e-4, norm-wise, for
+packed and padded calls, d = 64 (chain.hip) and d = 256 (chain2.hip); and asking for input
+gradients must leave the output and every parameter gradient bitwise unchanged.
+"""
+import numpy as np
+import pytest
+import torch
+
+from golden_util import model_args
+
+pytestmark = pytest.mark.gpu
+
+CASES = {
+    "d64_I2": dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=2, n_attn_layers=2, n_attn_hidden_dim=64,
+                   n_mlp_num_layers=3, n_mlp_hidden_dim=64, n_input_hidden_dim=64, n_expert=3, n_head=4,
+                   n_input_functions=2),
+    "d256_I1": dict(input_dim=3, theta_dim=2, input_func_dim=3, out_dim=1, n_attn_layers=1, n_attn_hidden_dim=256,
+                    n_mlp_num_layers=4, n_mlp_hidden_dim=256, n_input_hidden_dim=256, n_expert=2, n_head=8,
+                    n_input_functions=1),
+}
+
+
+def _rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+
+
+def _port_cfg(cfg):
+    return dict(cfg, d=cfg["n_attn_hidden_dim"])
+
+
+def _setup(name, seed=5):
+    from gnot_amd import GNOT
+    cfg = CASES[name]
+    torch.manual_seed(seed)
+    m = GNOT(*model_args(cfg)).cuda()
+    sd64 = {k: v.detach().double().cpu() for k, v in m.state_dict().items()}
+    return cfg, m, sd64
+
+
+def _port_grads(cfg, sd64, xs, thetas, fns_per_sample, Gs):
+    """float64 autograd of the port, one reference call per sample (packed offsets = B=1 calls)."""
+    from oracle import torch_port
+    gx, gt, gf = [], [], []
+    for b in range(len(xs)):
+        x = torch.tensor(xs[b], dtype=torch.float64)[None].requires_grad_(True)
+        t = torch.tensor(thetas[b], dtype=torch.float64)[None].requires_grad_(True)
+        fs = [torch.tensor(f, dtype=torch.float64)[None].requires_grad_(True) for f in fns_per_sample[b]]
+        out = torch_port.gnot_forward(sd64, _port_cfg(cfg), x, t, fs)
+        (out[0] * torch.tensor(Gs[b], dtype=torch.float64)).sum().backward()
+        gx.append(x.grad[0].numpy())
+        gt.append(t.grad[0].numpy())
+        gf.append([f.grad[0].numpy() for f in fs])
+    return gx, gt, gf
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_input_grads_packed_match_port(name):
+    cfg, m, sd64 = _setup(name)
+    I = cfg["n_input_functions"]
+    rng = np.random.default_rng(3)
+    Ns, Ms = [300, 173], [[120, 77], [64, 31]][:I]
+    xs = [rng.random((n, cfg["input_dim"])) for n in Ns]
+    thetas = [rng.random(cfg["theta_dim"]) for _ in Ns]
+    fns_ps = [[rng.random((Ms[i][b], cfg["input_func_dim"])) for i in range(I)] for b in range(len(Ns))]
+    Gs = [rng.standard_normal((n, cfg["out_dim"])) for n in Ns]
+
+    dev = torch.device("cuda")
+    x_off = [0, Ns[0], Ns[0] + Ns[1]]
+    fn_offs = [[0, Ms[i][0], Ms[i][0] + Ms[i][1]] for i in range(I)]
+    G = torch.tensor(np.concatenate(Gs), dtype=torch.float32, device=dev)
+
+    def run(want):
+        x = torch.tensor(np.concatenate(xs), dtype=torch.float32, device=dev).requires_grad_(want)
+        th = torch.tensor(np.stack(thetas), dtype=torch.float32, device=dev).requires_grad_(want)
+        fns = [torch.tensor(np.concatenate([fns_ps[b][i] for b in range(len(Ns))]), dtype=torch.float32,
+                            device=dev).requires_grad_(want) for i in range(I)]
+        m.zero_grad(set_to_none=True)
+        out = m.forward_packed(x, x_off, th, fns, fn_offs)
+        (out * G).sum().backward()
+        torch.cuda.synchronize()
+        pg = [p.grad.detach().clone() for p in m.parameters()]
+        return out.detach().clone(), pg, x.grad, th.grad, [f.grad for f in fns]
+
+    o0, pg0, _, _, _ = run(False)
+    o1, pg1, gx, gt, gf = run(True)
+    assert torch.equal(o0, o1)
+    assert all(torch.equal(a, b) for a, b in zip(pg0, pg1)), "input gradients changed a parameter gradient"
+
+    rx, rt, rf = _port_grads(cfg, sd64, xs, thetas, fns_ps, Gs)
+    e_x = _rel(gx.double().cpu().numpy(), np.concatenate(rx))
+    e_t = _rel(gt.double().cpu().numpy(), np.stack(rt))
+    assert e_x < 1e-4 and e_t < 1e-4, (e_x, e_t)
+    for i in range(I):
+        e_f = _rel(gf[i].double().cpu().numpy(), np.concatenate([rf[b][i] for b in range(len(Ns))]))
+        assert e_f < 1e-4, (i, e_f)
+
+
+def test_input_grads_padded_call_match_port():
+    """The reference calling convention (padded [B, N, in] batch, stacked [I, B, M, F] input functions,
+    main.py:60-89): gradients reach the padded tensors, pad rows included, as in the reference."""
+    from oracle import torch_port
+    cfg, m, sd64 = _setup("d64_I2", seed=9)
+    rng = np.random.default_rng(11)
+    B, N, M, I = 2, 96, 40, cfg["n_input_functions"]
+    x = rng.random((B, N, cfg["input_dim"]))
+    x[1, 70:] = 0.0                                   # zero-padded tail of the shorter sample
+    th = rng.random((B, cfg["theta_dim"]))
+    fns = rng.random((I, B, M, cfg["input_func_dim"]))
+    G = rng.standard_normal((B, N, cfg["out_dim"]))
+    dev = torch.device("cuda")
+    xg = torch.tensor(x, dtype=torch.float32, device=dev).requires_grad_(True)
+    tg = torch.tensor(th, dtype=torch.float32, device=dev).requires_grad_(True)
+    fg = torch.tensor(fns, dtype=torch.float32, device=dev).requires_grad_(True)
+    out = m(xg, tg, fg)
+    (out * torch.tensor(G, dtype=torch.float32, device=dev)).sum().backward()
+    torch.cuda.synchronize()
+    xr = torch.tensor(x).requires_grad_(True)
+    tr = torch.tensor(th).requires_grad_(True)
+    fr = torch.tensor(fns).requires_grad_(True)
+    ref = torch_port.gnot_forward(sd64, _port_cfg(cfg), xr, tr, [fr[i] for i in range(I)])
+    (ref * torch.tensor(G)).sum().backward()
+    for got, want in ((xg.grad, xr.grad), (tg.grad, tr.grad), (fg.grad, fr.grad)):
+        e = _rel(got.double().cpu().numpy(), want.numpy())
+        assert e < 1e-4, e

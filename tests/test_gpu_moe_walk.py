@@ -13,13 +13,14 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _run(monkeypatch, walk, recompute, E, I, d=256):
+def _run(monkeypatch, walk, recompute, E, I, d=256, prec="fp32"):
     from gnot_amd import GNOT
     monkeypatch.setenv("GNOT_MOE_WALK", walk)
     dev = torch.device("cuda")
     torch.manual_seed(17)
     model = GNOT(3, 1, 3, 1, 2, d, 4, d, d, E, 8, I).to(dev)
     model.set_moe_recompute(recompute)
+    model.set_precision(prec)
     g = torch.Generator(device="cpu").manual_seed(18)
     x_off = [0, 1500, 2093]                      # a partial last workgroup (2093 % 128 != 0)
     x = torch.rand(x_off[-1], 3, generator=g).to(dev)
@@ -33,11 +34,13 @@ def _run(monkeypatch, walk, recompute, E, I, d=256):
     return out.detach().clone(), [p.grad.detach().clone() for p in model.parameters()]
 
 
-@pytest.mark.parametrize("E,I", [(8, 1), (3, 0), (2, 2)])
-def test_walk_form_bitwise_equals_expert_grid(monkeypatch, E, I):
-    o0, g0 = _run(monkeypatch, "0", False, E, I)
-    o1, g1 = _run(monkeypatch, "1", False, E, I)
-    o2, g2 = _run(monkeypatch, "1", True, E, I)
+@pytest.mark.parametrize("E,I,prec", [(8, 1, "fp32"), (3, 0, "fp32"), (2, 2, "fp32"), (8, 1, "bf16"), (3, 0, "bf16")])
+def test_walk_form_bitwise_equals_expert_grid(monkeypatch, E, I, prec):
+    """prec "bf16": the bf16 mode, whose MoE chains store bf16 saves / dZ / Linear inputs (ChainArgs.b16s)
+    and whose MoE weight gradients run on pgemm_b16_kernel: the same equalities hold"""
+    o0, g0 = _run(monkeypatch, "0", False, E, I, prec=prec)
+    o1, g1 = _run(monkeypatch, "1", False, E, I, prec=prec)
+    o2, g2 = _run(monkeypatch, "1", True, E, I, prec=prec)
     assert torch.isfinite(o0).all()
     diff = lambda a, b: f"max |diff| {float((a - b).abs().max()):.3e} of max {float(a.abs().max()):.3e}"
     assert torch.equal(o0, o1), "walk output: " + diff(o0, o1)

@@ -8,12 +8,14 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("d,E,I", [(256, 8, 1), (64, 3, 0), (64, 2, 2)])
-def test_recompute_matches_saved_activations_bitwise(d, E, I):
+@pytest.mark.parametrize("d,E,I,prec", [(256, 8, 1, "fp32"), (64, 3, 0, "fp32"), (64, 2, 2, "fp32"), (256, 8, 1, "bf16")])
+def test_recompute_matches_saved_activations_bitwise(d, E, I, prec):
+    """prec "bf16": the bf16 mode's bf16 activation storage (the recompute rewrites the same bf16 saves)"""
     from gnot_amd import GNOT
     dev = torch.device("cuda")
     torch.manual_seed(7)
     model = GNOT(3, 1, 3, 1, 2, d, 4, d, d, E, 8 if d == 256 else 4, I).to(dev)
+    model.set_precision(prec)
     g = torch.Generator(device="cpu").manual_seed(8)
     x_off = [0, 1500, 2048]
     x = torch.rand(x_off[-1], 3, generator=g).to(dev)
