@@ -669,27 +669,16 @@ static hipError_t launch_chain2_d(const ChainArgs& a, bool bwd, hipStream_t s) {
   return hipErrorInvalidValue;
 }
 
-// Walk form or one workgroup per (point block, expert): the walk form has E x fewer, E x longer
-// workgroups (one per CU: 82 KiB LDS), so its last round of workgroups can leave CUs idle where the
-// expert grid fills them; the expert grid pays the [P, E, d] stage and the combine pass instead
-// (~7 % of the MoE forward at configs[2]).  Walk when its CU-round efficiency is within 10 % of the
-// expert grid's.  env GNOT_MOE_WALK = 0 / 1 forces either (read per call: the tests run both).
+// Walk form or one workgroup per (point block, expert).  Measured on one box at configs[2] (262,144
+// points, E = 8, interleaved runs, profiles/r03h_* and r03f_*): the expert grid + moe_combine takes
+// 233.0 ms per fp32 step against 236.2 for the walk form, and 112 against 127 ms in bf16 mode: the walk
+// form's E pipeline restarts per workgroup and its E x longer workgroups cost more than the [P, E, d]
+// stage and the combine pass.  So the grid is the default; env GNOT_MOE_WALK = 1 selects the walk form
+// (read per call: the tests run both, and they are bitwise equal).
 bool chain2_walk_choice(long P, int E) {
-  if (const char* env = std::getenv("GNOT_MOE_WALK")) {
-    if (env[0] == '0') return false;
-    if (env[0] == '1') return true;
-  }
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                 hipSuccess || cus <= 0)
-      cus = 256;
-  }
-  if (E < 2) return false;
-  const long blk = (P + 16 * kC2Waves - 1) / (16 * kC2Waves);
-  auto eff = [&](long wgs) { return (double)wgs / (double)(((wgs + cus - 1) / cus) * cus); };
-  return eff(blk) >= 0.9 * eff(blk * E);
+  (void)P;
+  const char* env = std::getenv("GNOT_MOE_WALK");
+  return env && env[0] == '1' && E >= 2;
 }
 
 hipError_t launch_chain2(const ChainArgs& a, bool bwd, hipStream_t s) {

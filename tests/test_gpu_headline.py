@@ -14,8 +14,8 @@ the 262,144-point bench takes:
   256 workgroups: 6 splits per MoE job group of 40 Linears, 51 per single-chain group of 5), and an
   odd number of 16-point stages in the last split (70,000 - 5 * 11,680 = 11,600 points = 725
   stages), the case of the stage-buffer reuse the db column sums once raced on;
-* the soft-MoE walk form (forced: GNOT_MOE_WALK=1; the bench's 262,144 points select it
-  automatically) and the expert grid;
+* the soft-MoE expert grid + moe_combine (the default the bench runs) and the walk form
+  (GNOT_MOE_WALK=1);
 * 70,000 is not a multiple of 128 (a partial last chain workgroup) nor of 256 (a partial state block).
 
 Checked against the float64 CPU oracle (oracle/gnot_oracle.py, pinned to the reference fixtures):
@@ -50,8 +50,8 @@ def mid_case():
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("walk", ["1", "0"])
 def test_configs2_widths_70k_points_fp32(mid_case, walk, monkeypatch):
-    """walk "1": the soft-MoE walk form the 262,144-point bench selects (at 70,000 points the automatic
-    choice is the expert grid, chain2_walk_choice); "0": the expert grid + moe_combine."""
+    """walk "0": the expert grid + moe_combine (the default, chain2_walk_choice); "1": the soft-MoE walk
+    form (GNOT_MOE_WALK=1)."""
     monkeypatch.setenv("GNOT_MOE_WALK", walk)
     fx, G = mid_case
     m = build_model(fx["params"], fx["cfg"])

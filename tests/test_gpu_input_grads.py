@@ -21,22 +21,16 @@ from golden_util import model_args
 pytestmark = pytest.mark.gpu
 
 CASES = {
-    "d64_I2": dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=2, n_attn_layers=2, n_attn_hidden_dim=64,
-                   n_mlp_num_layers=3, n_mlp_hidden_dim=64, n_input_hidden_dim=64, n_expert=3, n_head=4,
-                   n_input_functions=2),
-    "d256_I1": dict(input_dim=3, theta_dim=2, input_func_dim=3, out_dim=1, n_attn_layers=1, n_attn_hidden_dim=256,
-                    n_mlp_num_layers=4, n_mlp_hidden_dim=256, n_input_hidden_dim=256, n_expert=2, n_head=8,
-                    n_input_functions=1),
+    "d64_I2": dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=2, n_attn_layers=2, d=64,
+                   n_mlp_num_layers=3, n_expert=3, n_head=4, n_input_functions=2),
+    "d256_I1": dict(input_dim=3, theta_dim=2, input_func_dim=3, out_dim=1, n_attn_layers=1, d=256,
+                    n_mlp_num_layers=4, n_expert=2, n_head=8, n_input_functions=1),
 }
 
 
 def _rel(a, b):
     a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
-
-
-def _port_cfg(cfg):
-    return dict(cfg, d=cfg["n_attn_hidden_dim"])
 
 
 def _setup(name, seed=5):
@@ -56,7 +50,7 @@ def _port_grads(cfg, sd64, xs, thetas, fns_per_sample, Gs):
         x = torch.tensor(xs[b], dtype=torch.float64)[None].requires_grad_(True)
         t = torch.tensor(thetas[b], dtype=torch.float64)[None].requires_grad_(True)
         fs = [torch.tensor(f, dtype=torch.float64)[None].requires_grad_(True) for f in fns_per_sample[b]]
-        out = torch_port.gnot_forward(sd64, _port_cfg(cfg), x, t, fs)
+        out = torch_port.gnot_forward(sd64, cfg, x, t, fs)
         (out[0] * torch.tensor(Gs[b], dtype=torch.float64)).sum().backward()
         gx.append(x.grad[0].numpy())
         gt.append(t.grad[0].numpy())
@@ -128,7 +122,7 @@ def test_input_grads_padded_call_match_port():
     xr = torch.tensor(x).requires_grad_(True)
     tr = torch.tensor(th).requires_grad_(True)
     fr = torch.tensor(fns).requires_grad_(True)
-    ref = torch_port.gnot_forward(sd64, _port_cfg(cfg), xr, tr, [fr[i] for i in range(I)])
+    ref = torch_port.gnot_forward(sd64, cfg, xr, tr, [fr[i] for i in range(I)])
     (ref * torch.tensor(G)).sum().backward()
     for got, want in ((xg.grad, xr.grad), (tg.grad, tr.grad), (fg.grad, fr.grad)):
         e = _rel(got.double().cpu().numpy(), want.numpy())

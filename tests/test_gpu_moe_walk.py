@@ -48,3 +48,4 @@ def test_walk_form_bitwise_equals_expert_grid(monkeypatch, E, I, prec):
     for k, (a, b, c) in enumerate(zip(g0, g1, g2)):
         assert torch.equal(a, b), f"parameter {k}: walk differs from the expert grid, " + diff(a, b)
         assert torch.equal(a, c), f"parameter {k}: walk + recompute differs from the expert grid, " + diff(a, c)
+
