@@ -304,9 +304,19 @@ __global__ void __launch_bounds__(256) attn_kv_bwd_batch_kernel(const AttnKVBwdA
   switch (DHV) {                        \
     case 4: { constexpr int DH = 4; __VA_ARGS__; } break;    \
     case 8: { constexpr int DH = 8; __VA_ARGS__; } break;    \
+    case 12: { constexpr int DH = 12; __VA_ARGS__; } break;  \
     case 16: { constexpr int DH = 16; __VA_ARGS__; } break;  \
+    case 20: { constexpr int DH = 20; __VA_ARGS__; } break;  \
+    case 24: { constexpr int DH = 24; __VA_ARGS__; } break;  \
+    case 28: { constexpr int DH = 28; __VA_ARGS__; } break;  \
     case 32: { constexpr int DH = 32; __VA_ARGS__; } break;  \
+    case 36: { constexpr int DH = 36; __VA_ARGS__; } break;  \
+    case 40: { constexpr int DH = 40; __VA_ARGS__; } break;  \
+    case 44: { constexpr int DH = 44; __VA_ARGS__; } break;  \
     case 48: { constexpr int DH = 48; __VA_ARGS__; } break;  \
+    case 52: { constexpr int DH = 52; __VA_ARGS__; } break;  \
+    case 56: { constexpr int DH = 56; __VA_ARGS__; } break;  \
+    case 60: { constexpr int DH = 60; __VA_ARGS__; } break;  \
     case 64: { constexpr int DH = 64; __VA_ARGS__; } break;  \
     default: return hipErrorInvalidValue;                    \
   }

@@ -244,10 +244,18 @@ static hipError_t launch_chain(const ChainArgs& a, bool bwd, hipStream_t s) {
   if (a.P <= 0 || a.nchains <= 0) return hipSuccess;
   if (a.nlin < 2) return hipErrorInvalidValue;
   switch (a.D) {
+    case 16: return launch_chain_d<16>(a, bwd, s);
     case 32: return launch_chain_d<32>(a, bwd, s);
     case 48: return launch_chain_d<48>(a, bwd, s);
     case 64: return launch_chain_d<64>(a, bwd, s);
+    case 80: return launch_chain_d<80>(a, bwd, s);
+    case 96: return launch_chain_d<96>(a, bwd, s);
+    case 112: return launch_chain_d<112>(a, bwd, s);
     case 128: return launch_chain_d<128>(a, bwd, s);
+    case 144: return launch_chain_d<144>(a, bwd, s);
+    case 160: return launch_chain_d<160>(a, bwd, s);
+    case 176: return launch_chain_d<176>(a, bwd, s);
+    case 192: return launch_chain_d<192>(a, bwd, s);
     default: return hipErrorInvalidValue;
   }
 }

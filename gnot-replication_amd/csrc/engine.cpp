@@ -277,10 +277,13 @@ extern "C" int gnot_plan_create(const gnot_config* cfg, gnot_plan** out) {
   if (c.n_head <= 0 || D % c.n_head != 0)
     return fail(GNOT_E_INVALID, "n_embed should be divisible by head");   // model.py:41
   const int dh = D / c.n_head;
-  if (!(D == 32 || D == 48 || D == 64 || D == 128 || D == 256))
-    return fail(GNOT_E_INVALID, "hidden width must be one of 32, 48, 64, 128, 256 on the MI355X kernels");
-  if (!(dh == 4 || dh == 8 || dh == 16 || dh == 32 || dh == 48 || dh == 64))
-    return fail(GNOT_E_INVALID, "head width d/n_head must be one of 4, 8, 16, 32, 48, 64");
+  // chain.hip / linear.hip run any multiple of 16 up to 192 (whole 16-wide MFMA tiles, activations in
+  // registers), chain2.hip / linear2.hip d = 256; the attention passes any head width that is a multiple
+  // of 4 up to 64 (4-aligned lane slices, attn.hip; the fp32-MFMA forms at 16 / 32 / 64)
+  if (!((D % 16 == 0 && D >= 16 && D <= 192) || D == 256))
+    return fail(GNOT_E_INVALID, "hidden width must be a multiple of 16 up to 192, or 256, on the MI355X kernels");
+  if (dh % 4 != 0 || dh > 64)
+    return fail(GNOT_E_INVALID, "head width d/n_head must be a multiple of 4 up to 64 on the MI355X kernels");
   if (c.n_expert < 1 || c.n_attn_layers < 0 || c.n_input_functions < 0 || c.n_input_functions > 8)
     return fail(GNOT_E_INVALID, "bad n_expert / n_attn_layers / n_input_functions");
   if (c.input_dim + c.theta_dim > D || c.input_dim > D || c.input_func_dim > D || c.out_dim > D ||
@@ -1539,7 +1542,7 @@ int run_wgrad_side(Ctx& c, const WgradGroup& G, std::initializer_list<const floa
   // "capture fault".
   if (serial || c.s == p->side2) {
     float* slab = c.s == p->side2 ? p->P_("slab_wgrad2") : p->P_("slab_wgrad");
-    ProfScope ps(c, "wgrad", group_flops(G));
+    ProfScope ps(c, G.b16 ? "wgrad_b16" : "wgrad", group_flops(G));
     GNOT_RUN(launch_group(c.p, G, slab, c.s));
     return GNOT_OK;
   }
@@ -1547,7 +1550,8 @@ int run_wgrad_side(Ctx& c, const WgradGroup& G, std::initializer_list<const floa
   GNOT_CK(hipEventRecord(fork, c.s));
   GNOT_CK(hipStreamWaitEvent(p->side, fork, 0));
   {
-    ProfScope ps(c, "wgrad", group_flops(G), p->side);
+    // profiled as its own class: the bf16-row MoE weight gradients are HBM-bound, the others are not
+    ProfScope ps(c, G.b16 ? "wgrad_b16" : "wgrad", group_flops(G), p->side);
     GNOT_RUN(launch_group(p, G, p->P_("slab_wgrad"), p->side));
   }
   hipEvent_t done = next_event(p);

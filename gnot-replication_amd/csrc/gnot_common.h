@@ -544,7 +544,7 @@ GNOT_DEV void acc_to_regs(const f32x4 (&acc)[OT], float (&h)[OT][4]) {
 // Feature softmax over heads of `dh` consecutive features (model.py:59, 72, 93) applied to the
 // point-form tile set h[OT][4] (features 16T + 4g + r).  Supported: dh = 4, 8 or a multiple of 16.
 template <int OT>
-GNOT_DEV void softmax_heads(float (&h)[OT][4], int dh) {
+GNOT_DEV void softmax_heads(float (&h)[OT][4], int dh, int g) {
   if (dh == 4) {
 #pragma unroll
     for (int T = 0; T < OT; ++T) {
@@ -568,6 +568,39 @@ GNOT_DEV void softmax_heads(float (&h)[OT][4], int dh) {
       const float inv = 1.0f / s;
 #pragma unroll
       for (int r = 0; r < 4; ++r) h[T][r] *= inv;
+    }
+  } else if ((dh & 15) != 0) {
+    // any other dh (a multiple of 4): the 4 features of tile T in lane group g, 16T + 4g .. +3, lie in
+    // ONE head, (16T + 4g) / dh (the chunk starts at a head boundary, linear.hip linear_oc).  Per head:
+    // this lane's max / sum over its groups in the head, then a butterfly over the 4 lane groups of the
+    // point (a lane with no feature of the head contributes -inf / 0)
+    int hT[OT];
+#pragma unroll
+    for (int T = 0; T < OT; ++T) hT[T] = (16 * T + 4 * g) / dh;
+    const int nh = 16 * OT / dh;
+    for (int hd = 0; hd < nh; ++hd) {
+      float m = -INFINITY;
+#pragma unroll
+      for (int T = 0; T < OT; ++T)
+        if (hT[T] == hd) m = fmaxf(m, fmaxf(fmaxf(h[T][0], h[T][1]), fmaxf(h[T][2], h[T][3])));
+      m = fmaxf(m, shfl_xor(m, 16));
+      m = fmaxf(m, shfl_xor(m, 32));
+      float s = 0.f;
+#pragma unroll
+      for (int T = 0; T < OT; ++T)
+        if (hT[T] == hd) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) { h[T][r] = __expf(h[T][r] - m); s += h[T][r]; }
+        }
+      s += shfl_xor(s, 16);
+      s += shfl_xor(s, 32);
+      const float inv = 1.0f / s;
+#pragma unroll
+      for (int T = 0; T < OT; ++T)
+        if (hT[T] == hd) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) h[T][r] *= inv;
+        }
     }
   } else {
     const int tph = dh >> 4;  // tiles per head

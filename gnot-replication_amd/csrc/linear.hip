@@ -61,7 +61,7 @@ GNOT_DEV void linear_body(const LinearArgs& a, float4* wlds) {
   }
   float h[OC][4];
   acc_to_regs<OC>(acc, h);
-  if (c * 16 * OC < a.nsoft) softmax_heads<OC>(h, a.dh);
+  if (c * 16 * OC < a.nsoft) softmax_heads<OC>(h, a.dh, lane >> 4);
   float* Y = a.Y + c * 16 * OC;
   if (a.epi == EPI_ACCUM) {
     float old[OC][4];
@@ -93,8 +93,8 @@ __global__ void __launch_bounds__(256) linear_batch_kernel(const LinearArgs* __r
 // projection is ~1,250 waves at 4 tiles, 2,500 at 2), but the input rows are re-read once per chunk
 // and the extra waves compete with the side-stream weight-gradient GEMMs: measured at cfg2, 4 tiles
 // 3.57 ms/step, 8 tiles 3.74, 2 tiles 3.75, 1 tile 4.00.
-// GNOT_LINEAR_OC overrides the choice (experiments); a choice that does not tile D and NO, or that
-// would split a softmax head (dh > 16 * oc), falls back to the widest valid one.
+// GNOT_LINEAR_OC overrides the choice (experiments); a choice that does not tile D and NO, or whose
+// chunks would split a softmax head (16 * oc not a multiple of dh), falls back to the widest valid one.
 static int linear_oc(int D, int NO, int nsoft, int dh) {
   static const int env = [] {
     const char* e = getenv("GNOT_LINEAR_OC");
@@ -102,7 +102,7 @@ static int linear_oc(int D, int NO, int nsoft, int dh) {
   }();
   const int kt = D / 16;
   auto ok = [&](int oc) {
-    return oc >= 1 && oc <= 8 && kt % oc == 0 && NO % (16 * oc) == 0 && (nsoft == 0 || dh <= 16 * oc);
+    return oc >= 1 && oc <= 8 && kt % oc == 0 && NO % (16 * oc) == 0 && (nsoft == 0 || (16 * oc) % dh == 0);
   };
   int want = env > 0 ? env : 4;
   if (ok(want)) return want;
@@ -111,10 +111,14 @@ static int linear_oc(int D, int NO, int nsoft, int dh) {
   return 1;
 }
 
-#define GNOT_LIN_CASES                                                                          \
-  GNOT_LIN(32, 1) GNOT_LIN(32, 2) GNOT_LIN(48, 1) GNOT_LIN(48, 3) GNOT_LIN(64, 1) GNOT_LIN(64, 2) \
-  GNOT_LIN(64, 4) GNOT_LIN(128, 1) GNOT_LIN(128, 2) GNOT_LIN(128, 4) GNOT_LIN(128, 8) GNOT_LIN(256, 1)             \
-  GNOT_LIN(256, 2) GNOT_LIN(256, 4) GNOT_LIN(256, 8)
+// every (D, oc) linear_oc can return: oc a divisor of D / 16 (<= 8)
+#define GNOT_LIN_CASES                                                                                  \
+  GNOT_LIN(16, 1) GNOT_LIN(32, 1) GNOT_LIN(32, 2) GNOT_LIN(48, 1) GNOT_LIN(48, 3) GNOT_LIN(64, 1)         \
+  GNOT_LIN(64, 2) GNOT_LIN(64, 4) GNOT_LIN(80, 1) GNOT_LIN(80, 5) GNOT_LIN(96, 1) GNOT_LIN(96, 2)         \
+  GNOT_LIN(96, 3) GNOT_LIN(96, 6) GNOT_LIN(112, 1) GNOT_LIN(112, 7) GNOT_LIN(128, 1) GNOT_LIN(128, 2)     \
+  GNOT_LIN(128, 4) GNOT_LIN(128, 8) GNOT_LIN(144, 1) GNOT_LIN(144, 3) GNOT_LIN(160, 1) GNOT_LIN(160, 2)   \
+  GNOT_LIN(160, 5) GNOT_LIN(176, 1) GNOT_LIN(192, 1) GNOT_LIN(192, 2) GNOT_LIN(192, 3) GNOT_LIN(192, 4)   \
+  GNOT_LIN(192, 6) GNOT_LIN(256, 1) GNOT_LIN(256, 2) GNOT_LIN(256, 4) GNOT_LIN(256, 8)
 
 hipError_t launch_linear(const LinearArgs& a, int D, hipStream_t s) {
   if (a.P <= 0) return hipSuccess;

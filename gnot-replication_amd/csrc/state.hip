@@ -28,7 +28,10 @@ GNOT_DEV int find_job_s(const int* __restrict__ prefix, int njobs, int idx) {
   return lo;
 }
 
-constexpr int kMaxBlk = 4;   // 4x4 output blocks per thread: H*(dh/4)^2 <= 1024 (d <= 256, dh <= 64)
+constexpr int kMaxBlk = 4;
+// floats of one row-stage region: pts * d rounded up to whole 64-lane x 16-byte DMA instructions
+// (d > 128 takes pts = 8192 / d, e.g. 56 points x 144 = 8,064 floats: 31.5 instructions)
+__host__ __device__ constexpr int state_stage_floats(int pts, int d) { return (pts * d + 255) / 256 * 256; }   // 4x4 output blocks per thread: H*(dh/4)^2 <= 1024 (d <= 256, dh <= 64)
 
 // One workgroup = state_pts(d) points of one job.  The workgroup first pulls all of its A and B
 // rows into LDS with LDS-DMA (global_load_lds, 16 B per lane, every load in flight at once: one
@@ -50,9 +53,12 @@ __global__ void __launch_bounds__(kStateThreads) state_partial_kernel(const Wgra
   const int np = (int)min((long)pts, (long)J.P - p0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bool use_w = J.w != nullptr;
+  // each stage region is whole 1 KiB LDS-DMA wave-instructions (state_stage_floats): the last
+  // instruction of a stage writes all 64 lanes, so an unrounded region would spill into the next one
+  const int stage_f = state_stage_floats(pts, d);
   float* As = lds;
-  float* Bs = lds + pts * d;
-  float* Ws = lds + 2 * pts * d;
+  float* Bs = lds + stage_f;
+  float* Ws = lds + 2 * stage_f;
   float* S = slab + J.slab_off + (long)split * per;
   if (np > 0) {
     // ---- rows -> LDS (flat float4 index f of the [np, d] stage; lanes past the end re-read the last float4)
@@ -275,9 +281,10 @@ hipError_t launch_state(const WgradJob* jobs_dev, const int* wg_prefix_dev, int 
                        njobs, total_red, (const float*)slab);
     return hipGetLastError();
   }
-  // dynamic LDS, exactly what the workgroup stages: A and B rows (pts * d floats each) + the
-  // per-(point, head) weights; the partial-state combine reuses the A/B region (256 x 20 floats)
-  const size_t lds = std::max<size_t>((size_t)(2 * pts * d + pts * nw), 256 * 20) * sizeof(float);
+  // dynamic LDS, what the workgroup stages: A and B rows (pts * d floats each, rounded up to whole
+  // DMA instructions) + the per-(point, head) weights; the partial-state combine reuses the A/B region
+  // (256 x 20 floats)
+  const size_t lds = std::max<size_t>((size_t)(2 * state_stage_floats(pts, d) + pts * nw), 256 * 20) * sizeof(float);
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(state_partial_kernel),

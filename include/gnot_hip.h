@@ -32,7 +32,7 @@ typedef struct gnot_plan gnot_plan; /* opaque */
 
 /* GNOT constructor arguments, reference model.py:143 (positional order of main.py:44).
  * n_attn_hidden_dim, n_mlp_hidden_dim and n_input_hidden_dim must be equal (the reference's
- * residual adds, model.py:131/137, require it); d % 16 == 0, d/n_head in {4, 8, 16, 32, 48, 64}. */
+ * residual adds, model.py:131/137, require it); d a multiple of 16 up to 192, or 256; d/n_head a multiple of 4 up to 64. */
 typedef struct gnot_config {
   int input_dim;
   int theta_dim;

@@ -1,0 +1,54 @@
+"""Hidden and head widths beyond the BASELINE configs: the reference accepts any n_embed divisible by
+n_head (model.py:41).  This core takes every hidden width d that is a multiple of 16 up to 192 (the
+chain.hip / linear.hip kernels, whole 16-wide MFMA tiles) and d = 256 (chain2.hip / linear2.hip), with
+any head width dh = d / H that is a multiple of 4 up to 64 (the attention passes split a head into
+4-aligned lane slices; the projections' feature softmax reduces a head that straddles 16-feature tiles
+across the 4 lane groups of a point, gnot_common.h softmax_heads).
+
+Each case is checked against the float64 oracle (oracle/gnot_oracle.py, pinned to the reference's
+fixtures) at north_star's 1e-4: output and every parameter gradient (golden_util.check_parity), on a
+packed two-sample batch with input functions where the case has them.  The head widths other than
+16 / 32 / 64 run the VALU attention forms only (no MFMA variant), so both the size-based choice and the
+forced-MFMA setting (attn_path) reach the same kernels for them."""
+import functools
+
+import pytest
+
+from golden_util import check_parity
+from test_gpu_parity import _random_case, attn_path, build_model, run_packed  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+
+
+def _cfg(d, H, E, I, L=1, nl=3, out=2):
+    return dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=out, n_attn_layers=L, d=d,
+                n_mlp_num_layers=nl, n_expert=E, n_head=H, n_input_functions=I)
+
+
+CASES = {
+    "d16_h4": _cfg(16, 4, 2, 1),          # dh 4, the narrowest hidden width
+    "d80_h5": _cfg(80, 5, 2, 0, L=2),     # dh 16 with an odd tile count (5 tiles)
+    "d96_h8": _cfg(96, 8, 3, 1),          # dh 12: heads straddle 16-feature tiles
+    "d112_h4": _cfg(112, 4, 2, 2),        # dh 28, two input functions
+    "d144_h3": _cfg(144, 3, 2, 1),        # dh 48 above d = 128
+    "d160_h8": _cfg(160, 8, 2, 1),        # dh 20
+    "d192_h8": _cfg(192, 8, 2, 0),        # dh 24, self-attention only
+    "d192_h6": _cfg(192, 6, 2, 1, nl=4),  # dh 32 (fp32-MFMA attention forms at d = 192)
+}
+
+
+@functools.lru_cache(maxsize=None)
+def _case(name):
+    """the oracle result of a case (computed once for both attention paths)"""
+    cfg = CASES[name]
+    Ms = [[120, 77], [64, 31]][: cfg["n_input_functions"]]
+    return _random_case(13, cfg, [300, 173], Ms)
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_width_vs_oracle(name, attn_path):
+    fx, G = _case(name)
+    m = build_model(fx["params"], fx["cfg"])
+    out, grads = run_packed(m, fx, G)
+    errs = check_parity(out, grads, fx)
+    assert not errs, errs
