@@ -149,7 +149,7 @@ static void exchange(std::mt19937& rng) {
 
 int main() {
   std::mt19937 rng(12345);
-  const int widths[] = {32, 48, 64, 128, 256};
+  const int widths[] = {16, 32, 48, 64, 96, 128, 144, 192, 256};
   for (int d : widths)
     for (int I = 0; I <= 2; ++I) {
       gnot_config c{};
@@ -161,7 +161,7 @@ int main() {
       c.n_attn_hidden_dim = c.n_mlp_hidden_dim = c.n_input_hidden_dim = d;
       c.n_mlp_num_layers = 2 + (d % 3);
       c.n_expert = d == 32 ? 2 : d == 48 ? 3 : d == 256 ? 8 : 4;
-      c.n_head = d == 48 ? 3 : d >= 64 ? 8 : 4;
+      c.n_head = d == 48 || d == 144 ? 3 : d >= 64 ? 8 : 4;   // 96 / 192: head width 12 / 24
       c.n_input_functions = I;
       exercise(c, rng);
     }
