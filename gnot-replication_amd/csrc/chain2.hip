@@ -37,6 +37,14 @@
 #ifndef GNOT_C2_AHEAD_B
 #define GNOT_C2_AHEAD_B true
 #endif
+#ifndef GNOT_C2_B16_WPE
+#define GNOT_C2_B16_WPE 0      // bf16-storage chain kernels: waves per SIMD asked of the register allocator (0: none)
+#endif
+#if GNOT_C2_B16_WPE
+#define GNOT_C2_WPE(B16_) __attribute__((amdgpu_waves_per_eu((B16_) ? GNOT_C2_B16_WPE : 1)))
+#else
+#define GNOT_C2_WPE(B16_)
+#endif
 
 namespace gnot {
 
@@ -200,7 +208,7 @@ GNOT_DEV void c2f_layer(C2Pipe& pp, const u32x4* W, const u32x4 (&in)[KBI][NP], 
 // B16 (bf16 mode, ChainArgs::b16s): bf16 pair-interleaved saves, plus each Linear's RNE bf16 input (the
 // split the MFMAs consume, stored as it is made) for the weight gradients
 template <int D, int KT0, int OTL, bool SAVE, int NP, bool WALK, bool B16 = false>
-__global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) {
+__global__ void __launch_bounds__(64 * kC2Waves) GNOT_C2_WPE(B16) chain2_fwd_kernel(ChainArgs a) {
   constexpr int DT = D / 16, KB = DT / 2, KB0 = (KT0 + 1) / 2;
   using LD = C2Lds<D, NP>;
   extern __shared__ __attribute__((aligned(16))) u32x4 c2lds[];
@@ -452,7 +460,7 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP],
 // in place (expert e > 0 reads back the partial this lane stored for e-1), no stage, no combine pass.
 // B16 (bf16 mode, ChainArgs::b16s): saves and dz as bf16 pair-interleaved rows
 template <int D, int KT0, int OTL, int NP, bool WALK, bool B16 = false>
-__global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) {
+__global__ void __launch_bounds__(64 * kC2Waves) GNOT_C2_WPE(B16) chain2_bwd_kernel(ChainArgs a) {
   constexpr int DT = D / 16, KB = DT / 2, KBL = (OTL + 1) / 2;
   using LD = C2Lds<D, NP>;
   extern __shared__ __attribute__((aligned(16))) u32x4 c2lds[];

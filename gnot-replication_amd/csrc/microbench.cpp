@@ -93,6 +93,15 @@ int main(int argc, char** argv) {
     std::printf("chain_fwd  bf16 E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
     t = time_us([&] { CK(launch_chain_bwd(b1, nullptr)); });
     std::printf("chain_bwd  bf16 E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
+    // bf16 storage (ChainArgs::b16s, the bf16-mode soft-MoE chains): bf16 saves / inputs / dZ rows
+    ChainArgs a2 = a1, b2 = b1;
+    a2.b16s = 1; a2.save_layer_stride = (long)P * D / 2; a2.save_chain_stride = (long)NL * P * D;
+    b2.b16s = 1; b2.save_layer_stride = a2.save_layer_stride; b2.save_chain_stride = a2.save_chain_stride;
+    b2.dz_layer_stride = (long)P * D / 2; b2.dz_chain_stride = (long)NL * P * D / 2;
+    t = time_us([&] { CK(launch_chain_fwd(a2, nullptr)); });
+    std::printf("chain_fwd  b16s E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
+    t = time_us([&] { CK(launch_chain_bwd(b2, nullptr)); });
+    std::printf("chain_bwd  b16s E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
   }
 
   for (int NO : {D, 3 * D}) {
