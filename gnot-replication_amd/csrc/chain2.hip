@@ -37,6 +37,9 @@
 #ifndef GNOT_C2_AHEAD_B
 #define GNOT_C2_AHEAD_B true
 #endif
+#ifndef GNOT_C2B_K
+#define GNOT_C2B_K 6           // bf16-storage backward: saved-row tile pairs requested this many pairs ahead (<= 6)
+#endif
 #ifndef GNOT_C2_B16_WPE
 #define GNOT_C2_B16_WPE 0      // bf16-storage chain kernels: waves per SIMD asked of the register allocator (0: none)
 #endif
@@ -63,7 +66,10 @@ struct C2Lds {
   static constexpr int WB = c2_tile_u4(D / 32, NP) * (c2f_pair<NP>() ? 2 : 1);
   static constexpr int kBias = 2 * WB;                  // offset of the bias buffers
   static constexpr int kHs = kBias + 2 * 64;            // offset of the saved-row slots
-  static constexpr int kBytes = (kHs + kC2Waves * 4 * 64) * 16;
+  // saved-row slots per wave: 4 (bf16x6), 8 at one piece (the bf16-storage backward keeps up to
+  // GNOT_C2B_K + 1 tile pairs in flight; a power of two dividing the 8 pairs of a layer)
+  static constexpr int kSlots = NP == 1 ? 8 : 4;
+  static constexpr int kBytes = (kHs + kC2Waves * kSlots * 64) * 16;
 };
 
 
@@ -369,7 +375,12 @@ template <int KBI, int NP, bool B16 = false>
 GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP], rsrc_t rh, rsrc_t rz, rsrc_t rh_next,
                         bool has_next_h, int voff, const u32x4* nextW, int next_n16, int pend0, float (&nx)[16][4]) {
   constexpr int DT = 16, TU = c2_tile_u4(KBI, NP);
-  u32x4* slots = pp.lds + C2Lds<256, NP>::kHs + pp.wave * 4 * 64;
+  constexpr int SL = C2Lds<256, NP>::kSlots;
+  // B16: pairs requested PK pairs ahead (pair m of a layer in slot m % SL; the next layer's pairs
+  // continue the numbering, SL divides the 8 pairs of a layer); fp32 saves: tiles two ahead
+  constexpr int PK = B16 ? GNOT_C2B_K : 1;
+  static_assert(!B16 || (PK >= 1 && PK + 2 <= SL), "slot ring too small for the prefetch distance");
+  u32x4* slots = pp.lds + C2Lds<256, NP>::kHs + pp.wave * SL * 64;
   const int g = pp.lane >> 4;
   f32x4 prev;
   // one part of tile o's epilogue (inside the next tile's MFMA stream): part 0 waits for the saved
@@ -392,8 +403,8 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP],
   };
   // the saved tile of tile o's epilogue, read from its slot
   auto read_h = [&](int o) {
-    if constexpr (B16) hb = lds_read8_issue(slots + ((o >> 1) & 3) * 64 + pp.lane, 8 * (o & 1));
-    else hc = lds_read16_issue(slots + (o & 3) * 64 + pp.lane);
+    if constexpr (B16) hb = lds_read8_issue(slots + ((o >> 1) % SL) * 64 + pp.lane, 8 * (o & 1));
+    else hc = lds_read16_issue(slots + (o % SL) * 64 + pp.lane);
   };
   // tile o's dz store is issued at the top of tile o+2, after that tile's DMAs: a counted wait only
   // retires the ops issued before the DMA it waits for, so each store gets two tiles to drain
@@ -401,8 +412,9 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP],
     if constexpr (B16) store_tile_b16(nx[o], rz, voff, o, g);
     else buf_store_f32x4(make_float4(nx[o][0], nx[o][1], nx[o][2], nx[o][3]), rz, voff + 64 * o);
   };
-  // does tile t request saved rows (fp32: tile t + 2; B16: at even t, pair t / 2 + 1)?
-  auto hdma = [&](int t) { return (!B16 || (t & 1) == 0) && (t + 2 < DT || has_next_h); };
+  // does tile t request saved rows (fp32: tile t + 2; B16: at even t, pair t / 2 + PK)?
+  auto hdma = [&](int t) { return B16 ? ((t & 1) == 0 && (t / 2 + PK < DT / 2 || has_next_h))
+                                      : (t + 2 < DT || has_next_h); };
   constexpr int S = 1;                                   // stores per tile
 #pragma unroll
   for (int o = 0; o < DT; ++o) {
@@ -418,14 +430,14 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP],
       if (o + 1 < DT) dma_image(nb, Wt + (size_t)(o + 1) * TU, TU, kC2Waves, pp.wave, pp.lane);
       else if (nextW) dma_image(nb, nextW, next_n16, kC2Waves, pp.wave, pp.lane);
       if constexpr (B16) {
-        const int m = (o + 2) >> 1;
+        const int m = o / 2 + PK;
         if ((o & 1) == 0) {
-          if (o + 2 < DT) dma16(rh, slots + (m & 3) * 64, voff + 16 * g, 64 * m);
-          else if (has_next_h) dma16(rh_next, slots + (m & 3) * 64, voff + 16 * g, 64 * (m - DT / 2));
+          if (m < DT / 2) dma16(rh, slots + (m % SL) * 64, voff + 16 * g, 64 * m);
+          else if (has_next_h) dma16(rh_next, slots + (m % SL) * 64, voff + 16 * g, 64 * (m - DT / 2));
         }
       } else {
-        if (o + 2 < DT) dma16(rh, slots + ((o + 2) & 3) * 64, voff, 64 * (o + 2));
-        else if (has_next_h) dma16(rh_next, slots + ((o + 2) & 3) * 64, voff, 64 * (o + 2 - DT));
+        if (o + 2 < DT) dma16(rh, slots + ((o + 2) % SL) * 64, voff, 64 * (o + 2));
+        else if (has_next_h) dma16(rh_next, slots + ((o + 2) % SL) * 64, voff, 64 * (o + 2 - DT));
       }
       if (o >= 2) stores(o - 2);
     };
@@ -490,13 +502,15 @@ __global__ void __launch_bounds__(64 * kC2Waves) GNOT_C2_WPE(B16) chain2_bwd_ker
   const unsigned lb = B16 ? lay_b16 : lay_bytes;
   auto rh = [&](int l) { return make_rsrc(save + l * a.save_layer_stride, lb); };   // h_l
   auto rz = [&](int l) { return make_rsrc(dz + l * a.dz_layer_stride, lb); };      // dz_l
-  // prologue DMA: the last Linear's tile-0 weights and the first two h_{nl-2} tiles (B16: pair 0)
+  // prologue DMA: the last Linear's tile-0 weights and the first two h_{nl-2} tiles (B16: pairs 0 ..
+  // GNOT_C2B_K - 1)
   dma_image(c2lds, wt(nl - 1), c2_tile_u4(KBL, NP), kC2Waves, wave, lane);
   {
-    u32x4* slots = c2lds + LD::kHs + wave * 4 * 64;
+    u32x4* slots = c2lds + LD::kHs + wave * LD::kSlots * 64;
     const rsrc_t r = rh(nl - 2);
     if constexpr (B16) {
-      dma16(r, slots, rowb + 16 * g, 0);
+#pragma unroll
+      for (int m = 0; m < GNOT_C2B_K; ++m) dma16(r, slots + m * 64, rowb + 16 * g, 64 * m);
     } else {
       dma16(r, slots, voff, 0);
       dma16(r, slots + 64, voff, 64);
