@@ -37,6 +37,9 @@
 #ifndef GNOT_C2_AHEAD_B
 #define GNOT_C2_AHEAD_B true
 #endif
+#ifndef GNOT_C2B_LEAD
+#define GNOT_C2B_LEAD 3        // backward: weight chunks in flight ahead of the one being consumed (1 .. kC2Ring - 1)
+#endif
 #ifndef GNOT_C2B_K
 #define GNOT_C2B_K 6           // bf16-storage backward: saved-row tile pairs requested this many pairs ahead (<= 6)
 #endif
@@ -51,7 +54,6 @@
 
 namespace gnot {
 
-constexpr int S_BWD = 1;   // vector-memory stores per backward tile (the dz tile)
 
 // LDS of one workgroup (u32x4 units): two weight-chunk buffers, two 1 KiB bias buffers (layer parity,
 // forward) and per wave four 1 KiB slots of saved pre-activation tiles (backward).
@@ -64,7 +66,7 @@ template <int D, int NP>
 struct C2Lds {
   // one weight chunk: one output tile of a D x D image (two in the forward's pair mode)
   static constexpr int WB = c2_tile_u4(D / 32, NP) * (c2f_pair<NP>() ? 2 : 1);
-  static constexpr int kBias = 2 * WB;                  // offset of the bias buffers
+  static constexpr int kBias = kC2Ring * WB;            // offset of the bias buffers
   static constexpr int kHs = kBias + 2 * 64;            // offset of the saved-row slots
   // saved-row slots per wave: 4 (bf16x6), 8 at one piece (the bf16-storage backward keeps up to
   // GNOT_C2B_K + 1 tile pairs in flight; a power of two dividing the 8 pairs of a layer)
@@ -365,16 +367,20 @@ __global__ void __launch_bounds__(64 * kC2Waves) GNOT_C2_WPE(B16) chain2_fwd_ker
 
 // ------------------------------------------------------------------------------------------ backward
 // One backward layer l: g = W_l^T dz_l (DT output tiles of the split input `in`), dz_{l-1} = g *
-// gelu'(h_{l-1}) stored (rz) and kept in nx.  The saved pre-activation tiles h_{l-1} arrive by LDS-DMA
-// two tiles ahead into this wave's four slots (tile o in slot o % 4; the next layer's tiles 0 and 1
-// are requested by this layer's last two tiles).  Entry: the layer's tile-0 weights in pp.cur(), its
-// h tiles 0 and 1 requested, `pend0` vector-memory ops issued after its tile-0 weight DMA.
+// gelu'(h_{l-1}) stored (rz) and kept in nx.  Weight chunks stream through the ring GNOT_C2B_LEAD tiles
+// ahead (the last tiles request the next image's first chunks); each tile's wait retires its own chunk
+// and leaves every younger op of the wave in flight (C2Pipe::younger).  The saved pre-activation tiles
+// h_{l-1} arrive by LDS-DMA two tiles ahead into this wave's slots (tile o in slot o % kSlots; the next
+// layer's tiles 0 and 1 are requested by this layer's last two tiles).  Entry: the layer's first
+// GNOT_C2B_LEAD chunks and its h tiles 0 and 1 requested.
 // B16 (bf16 storage, voff = the lane's row * 512 B): h and dz are pair-interleaved bf16 rows; one 16-byte
 // DMA brings the h of a tile PAIR (pair m into slot m % 4, requested at tile 2m - 2), dz stores are 8 B
 template <int KBI, int NP, bool B16 = false>
 GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP], rsrc_t rh, rsrc_t rz, rsrc_t rh_next,
-                        bool has_next_h, int voff, const u32x4* nextW, int next_n16, int pend0, float (&nx)[16][4]) {
-  constexpr int DT = 16, TU = c2_tile_u4(KBI, NP);
+                        bool has_next_h, int voff, const u32x4* nextW, int next_n16, int next_tiles,
+                        float (&nx)[16][4]) {
+  constexpr int DT = 16, TU = c2_tile_u4(KBI, NP), LEAD = GNOT_C2B_LEAD;
+  static_assert(LEAD >= 1 && LEAD < kC2Ring, "weight ring too small");
   constexpr int SL = C2Lds<256, NP>::kSlots;
   // B16: pairs requested PK pairs ahead (pair m of a layer in slot m % SL; the next layer's pairs
   // continue the numbering, SL divides the 8 pairs of a layer); fp32 saves: tiles two ahead
@@ -411,24 +417,26 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP],
   auto stores = [&](int o) {
     if constexpr (B16) store_tile_b16(nx[o], rz, voff, o, g);
     else buf_store_f32x4(make_float4(nx[o][0], nx[o][1], nx[o][2], nx[o][3]), rz, voff + 64 * o);
+    ++pp.issued;
   };
   // does tile t request saved rows (fp32: tile t + 2; B16: at even t, pair t / 2 + PK)?
   auto hdma = [&](int t) { return B16 ? ((t & 1) == 0 && (t / 2 + PK < DT / 2 || has_next_h))
                                       : (t + 2 < DT || has_next_h); };
-  constexpr int S = 1;                                   // stores per tile
 #pragma unroll
   for (int o = 0; o < DT; ++o) {
-    // ops issued after the weight DMA this wait retires (at the top of tile o-1): that tile's h DMA
-    // (none when it would be past the next layer) and the stores of tile o-3
-    if (o == 0) c2_sync_n(pend0);
-    else c2_sync_n((hdma(o - 1) ? 1 : 0) + (o >= 3 ? S : 0));
-    const u32x4* cb = pp.cur();
-    u32x4* nb = pp.nxt();
-    ++pp.cnt;
-    // the weight chunk's DMA in its loop form (unrolled measured 149 -> 141 TFLOP/s)
+    // this tile's chunk (DMA'd LEAD tiles back): every op of this wave younger than it may stay in flight
+    // ring positions are static: every backward layer has 16 tiles and starts at buffer 0 (the mark
+    // array must only ever be indexed by constants, or it goes to scratch memory)
+    c2_sync_n(pp.issued - pp.mark[o % kC2Ring]);
+    const u32x4* cb = pp.lds + (o % kC2Ring) * pp.WB;
+    u32x4* nb = pp.lds + ((o + LEAD) % kC2Ring) * pp.WB;
+    const int nmark = (o + LEAD) % kC2Ring;
+    // the weight DMA of chunk o + LEAD (this layer's, or the next image's first tiles) in its loop form
+    // (unrolled measured 149 -> 141 TFLOP/s), then this tile's h DMA and the dz store of tile o - 2
+    // (h first: the counted wait of tile o + 1 retires only ops OLDER than chunk o + 1's weight DMA,
+    // issued LEAD tiles back, and must retire the h of tile o requested then too)
     auto issue = [&]() __attribute__((always_inline)) {
-      if (o + 1 < DT) dma_image(nb, Wt + (size_t)(o + 1) * TU, TU, kC2Waves, pp.wave, pp.lane);
-      else if (nextW) dma_image(nb, nextW, next_n16, kC2Waves, pp.wave, pp.lane);
+      if (hdma(o)) ++pp.issued;
       if constexpr (B16) {
         const int m = o / 2 + PK;
         if ((o & 1) == 0) {
@@ -439,6 +447,15 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP],
         if (o + 2 < DT) dma16(rh, slots + ((o + 2) % SL) * 64, voff, 64 * (o + 2));
         else if (has_next_h) dma16(rh_next, slots + ((o + 2) % SL) * 64, voff, 64 * (o + 2 - DT));
       }
+      const int t = o + LEAD;
+      if (t < DT) {
+        dma_image(nb, Wt + (size_t)t * TU, TU, kC2Waves, pp.wave, pp.lane);
+        pp.issued += dma_image_count(TU, kC2Waves, pp.wave);
+      } else if (nextW && t - DT < next_tiles) {
+        dma_image(nb, nextW + (size_t)(t - DT) * next_n16, next_n16, kC2Waves, pp.wave, pp.lane);
+        pp.issued += dma_image_count(next_n16, kC2Waves, pp.wave);
+      }
+      pp.mark[nmark] = pp.issued;
       if (o >= 2) stores(o - 2);
     };
     f32x4 acc;
@@ -502,18 +519,27 @@ __global__ void __launch_bounds__(64 * kC2Waves) GNOT_C2_WPE(B16) chain2_bwd_ker
   const unsigned lb = B16 ? lay_b16 : lay_bytes;
   auto rh = [&](int l) { return make_rsrc(save + l * a.save_layer_stride, lb); };   // h_l
   auto rz = [&](int l) { return make_rsrc(dz + l * a.dz_layer_stride, lb); };      // dz_l
-  // prologue DMA: the last Linear's tile-0 weights and the first two h_{nl-2} tiles (B16: pairs 0 ..
-  // GNOT_C2B_K - 1)
-  dma_image(c2lds, wt(nl - 1), c2_tile_u4(KBL, NP), kC2Waves, wave, lane);
+  // prologue DMA: the last Linear's first GNOT_C2B_LEAD weight chunks (ring buffers 0 ..) and the first
+  // two h_{nl-2} tiles (B16: pairs 0 .. GNOT_C2B_K - 1)
+  // (h first: a chunk's counted wait retires only the ops older than its DMA)
   {
     u32x4* slots = c2lds + LD::kHs + wave * LD::kSlots * 64;
     const rsrc_t r = rh(nl - 2);
     if constexpr (B16) {
 #pragma unroll
       for (int m = 0; m < GNOT_C2B_K; ++m) dma16(r, slots + m * 64, rowb + 16 * g, 64 * m);
+      pp.issued += GNOT_C2B_K;
     } else {
       dma16(r, slots, voff, 0);
       dma16(r, slots + 64, voff, 64);
+      pp.issued += 2;
+    }
+    constexpr int TU1 = c2_tile_u4(KBL, NP);
+#pragma unroll
+    for (int t = 0; t < GNOT_C2B_LEAD; ++t) {
+      dma_image(c2lds + t * LD::WB, wt(nl - 1) + (size_t)t * TU1, TU1, kC2Waves, wave, lane);
+      pp.issued += dma_image_count(TU1, kC2Waves, wave);
+      pp.mark[t] = pp.issued;
     }
   }
   // ---- gradient at the chain output
@@ -563,34 +589,37 @@ __global__ void __launch_bounds__(64 * kC2Waves) GNOT_C2_WPE(B16) chain2_bwd_ker
   u32x4 bp[KB][NP];
   // next image after layer l's tiles: layer l-1's W^T, or the first Linear's (dX) when l - 1 == 0
   auto next_img = [&](int l) -> const u32x4* { return (l - 1 >= 1 || a.dX) ? wt(l - 1) : nullptr; };
+  // output tiles of the next image (hidden Linear: DT; the first Linear's dX: KT0)
+  auto next_tiles = [&](int l) { return l - 1 >= 1 ? DT : KT0; };
   {
     u32x4 bl[KBL][NP];
     c2_split<OTL, NP>(dy, bl);
     const int l = nl - 1;
     c2b_layer<KBL, NP, B16>(pp, wt(l), bl, rh(l - 1), rz(l - 1), rh(l >= 2 ? l - 2 : 0), l - 1 >= 1, lvoff,
-                            next_img(l), c2_tile_u4(KB, NP), 0, nx);
+                            next_img(l), c2_tile_u4(KB, NP), next_tiles(l), nx);
   }
   for (int l = nl - 2; l >= 1; --l) {
     c2_split<DT, NP>(nx, bp);
-    // first wait: after the previous layer's last weight DMA, its h DMA (B16: none at the odd last
-    // tile) and the stores of its last three tiles
     c2b_layer<KB, NP, B16>(pp, wt(l), bp, rh(l - 1), rz(l - 1), rh(l >= 2 ? l - 2 : 0), l - 1 >= 1, lvoff,
-                           next_img(l), c2_tile_u4(KB, NP), (B16 ? 0 : 1) + 3 * S_BWD, nx);
+                           next_img(l), c2_tile_u4(KB, NP), next_tiles(l), nx);
   }
-  // ---- first Linear: dX = W_0^T dz_0 (KT0 output tiles); first wait: the stores of the last layer's
-  // last three tiles
+  // ---- first Linear: dX = W_0^T dz_0 (KT0 output tiles); its first GNOT_C2B_LEAD chunks were requested
+  // by the last layer above
   if (a.dX) {
     c2_split<DT, NP>(nx, bp);
     const u32x4* W0 = wt(0);
+    constexpr int TU0 = c2_tile_u4(KB, NP);
     float dx[KT0][4];
 #pragma unroll
     for (int o = 0; o < KT0; ++o) {
-      if (o == 0) c2_sync_n(3 * S_BWD);
-      else c2_sync<0>();
-      const u32x4* cb = pp.cur();
-      if (o + 1 < KT0)
-        dma_image(pp.nxt(), W0 + (size_t)(o + 1) * c2_tile_u4(KB, NP), c2_tile_u4(KB, NP), kC2Waves, wave, lane);
-      ++pp.cnt;
+      c2_sync_n(pp.issued - pp.mark[o % kC2Ring]);
+      const u32x4* cb = c2lds + (o % kC2Ring) * LD::WB;
+      if (o + GNOT_C2B_LEAD < KT0) {
+        dma_image(c2lds + ((o + GNOT_C2B_LEAD) % kC2Ring) * LD::WB, W0 + (size_t)(o + GNOT_C2B_LEAD) * TU0, TU0,
+                  kC2Waves, wave, lane);
+        pp.issued += dma_image_count(TU0, kC2Waves, wave);
+      }
+      pp.mark[(o + GNOT_C2B_LEAD) % kC2Ring] = pp.issued;
       f32x4 acc = c2_tile<KB, false, NP>(cb, bp, f32x4{0.f, 0.f, 0.f, 0.f}, lane);
 #pragma unroll
       for (int r = 0; r < 4; ++r) dx[o][r] = acc[r];

@@ -163,18 +163,36 @@ GNOT_DEV void c2_sync_n(int n) {   // n is wave-uniform and small
     case 10: c2_sync<10>(); break;
     case 11: c2_sync<11>(); break;
     case 12: c2_sync<12>(); break;
+    case 13: c2_sync<13>(); break;
+    case 14: c2_sync<14>(); break;
+    case 15: c2_sync<15>(); break;
+    case 16: c2_sync<16>(); break;
     default: c2_sync<0>(); break;
   }
 }
-// the double-buffered weight-chunk stream of a chain kernel (chain2.hip)
+// the weight-chunk stream of a chain kernel (chain2.hip): a ring of kC2Ring chunk buffers.  The
+// forward keeps one chunk in flight (nxt); the backward keeps GNOT_C2B_LEAD in flight and waits for a
+// chunk with a counted vmcnt: `issued` counts this wave's vector-memory ops as they are issued, mark[b] is
+// that count right after the DMA of the chunk in buffer b, so issued - mark[b] ops are younger than it
+constexpr int kC2Ring = 4;
 struct C2Pipe {
   u32x4* lds;
   int WB;
-  int cnt;          // weight chunks consumed (buffer parity)
+  int cnt;          // weight chunks consumed (ring position)
   int wave, lane;
-  GNOT_DEV const u32x4* cur() const { return lds + (cnt & 1) * WB; }
-  GNOT_DEV u32x4* nxt() const { return lds + ((cnt + 1) & 1) * WB; }
+  int issued = 0;
+  int mark[kC2Ring] = {0, 0, 0, 0};
+  GNOT_DEV const u32x4* cur() const { return lds + (cnt % kC2Ring) * WB; }
+  GNOT_DEV u32x4* nxt() const { return lds + ((cnt + 1) % kC2Ring) * WB; }
+  GNOT_DEV u32x4* at(int k) const { return lds + ((cnt + k) % kC2Ring) * WB; }
+  // vector-memory ops younger than the DMA of the chunk about to be consumed
+  GNOT_DEV int younger() const { return issued - mark[cnt % kC2Ring]; }
 };
+// this wave's instruction count of dma_image(lds, src, n16, nwaves, wave, lane)
+GNOT_DEV int dma_image_count(int n16, int nwaves, int wave) {
+  const int w = __builtin_amdgcn_readfirstlane(wave);
+  return w * 64 < n16 ? (n16 - w * 64 + nwaves * 64 - 1) / (nwaves * 64) : 0;
+}
 
 // LDS read of a slot this wave filled by LDS-DMA and already waited for with a counted vmcnt: inline
 // asm, so hipcc does not insert its own vmcnt(0) for the DMA still in flight to OTHER buffers (it cannot
