@@ -37,9 +37,16 @@
 #ifndef GNOT_C2_AHEAD_B
 #define GNOT_C2_AHEAD_B true
 #endif
-#ifndef GNOT_C2B_LEAD
-#define GNOT_C2B_LEAD 3        // backward: weight chunks in flight ahead of the one being consumed (1 .. kC2Ring - 1)
+// backward: weight chunks in flight ahead of the one being consumed (1 .. kC2Ring - 1), per arithmetic:
+// bf16x6 (NP = 3) and one-piece bf16 (NP = 1)
+#ifndef GNOT_C2B_LEAD_X6
+#define GNOT_C2B_LEAD_X6 1        // in-step (r03x): lead 1 232.2 ms, lead 2 235.0, lead 3 234.7 (concurrent weight gradients)
 #endif
+#ifndef GNOT_C2B_LEAD_B
+#define GNOT_C2B_LEAD_B 3
+#endif
+template <int NP>
+constexpr int c2b_lead() { return NP == 3 ? GNOT_C2B_LEAD_X6 : GNOT_C2B_LEAD_B; }
 #ifndef GNOT_C2B_K
 #define GNOT_C2B_K 6           // bf16-storage backward: saved-row tile pairs requested this many pairs ahead (<= 6)
 #endif
@@ -367,19 +374,19 @@ __global__ void __launch_bounds__(64 * kC2Waves) GNOT_C2_WPE(B16) chain2_fwd_ker
 
 // ------------------------------------------------------------------------------------------ backward
 // One backward layer l: g = W_l^T dz_l (DT output tiles of the split input `in`), dz_{l-1} = g *
-// gelu'(h_{l-1}) stored (rz) and kept in nx.  Weight chunks stream through the ring GNOT_C2B_LEAD tiles
+// gelu'(h_{l-1}) stored (rz) and kept in nx.  Weight chunks stream through the ring c2b_lead<NP>() tiles
 // ahead (the last tiles request the next image's first chunks); each tile's wait retires its own chunk
 // and leaves every younger op of the wave in flight (C2Pipe::younger).  The saved pre-activation tiles
 // h_{l-1} arrive by LDS-DMA two tiles ahead into this wave's slots (tile o in slot o % kSlots; the next
 // layer's tiles 0 and 1 are requested by this layer's last two tiles).  Entry: the layer's first
-// GNOT_C2B_LEAD chunks and its h tiles 0 and 1 requested.
+// c2b_lead<NP>() chunks and its h tiles 0 and 1 requested.
 // B16 (bf16 storage, voff = the lane's row * 512 B): h and dz are pair-interleaved bf16 rows; one 16-byte
 // DMA brings the h of a tile PAIR (pair m into slot m % 4, requested at tile 2m - 2), dz stores are 8 B
 template <int KBI, int NP, bool B16 = false>
 GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP], rsrc_t rh, rsrc_t rz, rsrc_t rh_next,
                         bool has_next_h, int voff, const u32x4* nextW, int next_n16, int next_tiles,
                         float (&nx)[16][4]) {
-  constexpr int DT = 16, TU = c2_tile_u4(KBI, NP), LEAD = GNOT_C2B_LEAD;
+  constexpr int DT = 16, TU = c2_tile_u4(KBI, NP), LEAD = c2b_lead<NP>();
   static_assert(LEAD >= 1 && LEAD < kC2Ring, "weight ring too small");
   constexpr int SL = C2Lds<256, NP>::kSlots;
   // B16: pairs requested PK pairs ahead (pair m of a layer in slot m % SL; the next layer's pairs
@@ -519,7 +526,7 @@ __global__ void __launch_bounds__(64 * kC2Waves) GNOT_C2_WPE(B16) chain2_bwd_ker
   const unsigned lb = B16 ? lay_b16 : lay_bytes;
   auto rh = [&](int l) { return make_rsrc(save + l * a.save_layer_stride, lb); };   // h_l
   auto rz = [&](int l) { return make_rsrc(dz + l * a.dz_layer_stride, lb); };      // dz_l
-  // prologue DMA: the last Linear's first GNOT_C2B_LEAD weight chunks (ring buffers 0 ..) and the first
+  // prologue DMA: the last Linear's first c2b_lead<NP>() weight chunks (ring buffers 0 ..) and the first
   // two h_{nl-2} tiles (B16: pairs 0 .. GNOT_C2B_K - 1)
   // (h first: a chunk's counted wait retires only the ops older than its DMA)
   {
@@ -536,7 +543,7 @@ __global__ void __launch_bounds__(64 * kC2Waves) GNOT_C2_WPE(B16) chain2_bwd_ker
     }
     constexpr int TU1 = c2_tile_u4(KBL, NP);
 #pragma unroll
-    for (int t = 0; t < GNOT_C2B_LEAD; ++t) {
+    for (int t = 0; t < c2b_lead<NP>(); ++t) {
       dma_image(c2lds + t * LD::WB, wt(nl - 1) + (size_t)t * TU1, TU1, kC2Waves, wave, lane);
       pp.issued += dma_image_count(TU1, kC2Waves, wave);
       pp.mark[t] = pp.issued;
@@ -603,7 +610,7 @@ __global__ void __launch_bounds__(64 * kC2Waves) GNOT_C2_WPE(B16) chain2_bwd_ker
     c2b_layer<KB, NP, B16>(pp, wt(l), bp, rh(l - 1), rz(l - 1), rh(l >= 2 ? l - 2 : 0), l - 1 >= 1, lvoff,
                            next_img(l), c2_tile_u4(KB, NP), next_tiles(l), nx);
   }
-  // ---- first Linear: dX = W_0^T dz_0 (KT0 output tiles); its first GNOT_C2B_LEAD chunks were requested
+  // ---- first Linear: dX = W_0^T dz_0 (KT0 output tiles); its first c2b_lead<NP>() chunks were requested
   // by the last layer above
   if (a.dX) {
     c2_split<DT, NP>(nx, bp);
@@ -614,12 +621,12 @@ __global__ void __launch_bounds__(64 * kC2Waves) GNOT_C2_WPE(B16) chain2_bwd_ker
     for (int o = 0; o < KT0; ++o) {
       c2_sync_n(pp.issued - pp.mark[o % kC2Ring]);
       const u32x4* cb = c2lds + (o % kC2Ring) * LD::WB;
-      if (o + GNOT_C2B_LEAD < KT0) {
-        dma_image(c2lds + ((o + GNOT_C2B_LEAD) % kC2Ring) * LD::WB, W0 + (size_t)(o + GNOT_C2B_LEAD) * TU0, TU0,
+      if (o + c2b_lead<NP>() < KT0) {
+        dma_image(c2lds + ((o + c2b_lead<NP>()) % kC2Ring) * LD::WB, W0 + (size_t)(o + c2b_lead<NP>()) * TU0, TU0,
                   kC2Waves, wave, lane);
         pp.issued += dma_image_count(TU0, kC2Waves, wave);
       }
-      pp.mark[(o + GNOT_C2B_LEAD) % kC2Ring] = pp.issued;
+      pp.mark[(o + c2b_lead<NP>()) % kC2Ring] = pp.issued;
       f32x4 acc = c2_tile<KB, false, NP>(cb, bp, f32x4{0.f, 0.f, 0.f, 0.f}, lane);
 #pragma unroll
       for (int r = 0; r < 4; ++r) dx[o][r] = acc[r];
