@@ -47,6 +47,13 @@
 #endif
 template <int NP>
 constexpr int c2b_lead() { return NP == 3 ? GNOT_C2B_LEAD_X6 : GNOT_C2B_LEAD_B; }
+#ifndef GNOT_C2B_PAIR
+#define GNOT_C2B_PAIR 1        // bf16-storage backward: two output tiles per weight chunk (one wait + barrier)
+#endif
+// output tiles per weight chunk of the backward (the bf16-storage chains' pair mode; the ring buffers
+// of the one-piece chains already hold two tiles, C2Lds::WB)
+template <int NP, bool B16>
+constexpr int c2b_ch() { return (B16 && NP == 1 && GNOT_C2B_PAIR) ? 2 : 1; }
 #ifndef GNOT_C2B_K
 #define GNOT_C2B_K 6           // bf16-storage backward: saved-row tile pairs requested this many pairs ahead (<= 6)
 #endif
@@ -386,8 +393,10 @@ template <int KBI, int NP, bool B16 = false>
 GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP], rsrc_t rh, rsrc_t rz, rsrc_t rh_next,
                         bool has_next_h, int voff, const u32x4* nextW, int next_n16, int next_tiles,
                         float (&nx)[16][4]) {
-  constexpr int DT = 16, TU = c2_tile_u4(KBI, NP), LEAD = c2b_lead<NP>();
+  constexpr int DT = 16, TU = c2_tile_u4(KBI, NP), LEAD = c2b_lead<NP>(), CH = c2b_ch<NP, B16>(), NC = DT / CH;
   static_assert(LEAD >= 1 && LEAD < kC2Ring, "weight ring too small");
+  static_assert(CH == 1 || (B16 && GNOT_C2B_K >= LEAD), "pair mode: a pair's saved rows must be requested no later "
+                                                         "than the chunk whose wait retires them");
   constexpr int SL = C2Lds<256, NP>::kSlots;
   // B16: pairs requested PK pairs ahead (pair m of a layer in slot m % SL; the next layer's pairs
   // continue the numbering, SL divides the 8 pairs of a layer); fp32 saves: tiles two ahead
@@ -431,13 +440,16 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP],
                                       : (t + 2 < DT || has_next_h); };
 #pragma unroll
   for (int o = 0; o < DT; ++o) {
-    // this tile's chunk (DMA'd LEAD tiles back): every op of this wave younger than it may stay in flight
-    // ring positions are static: every backward layer has 16 tiles and starts at buffer 0 (the mark
-    // array must only ever be indexed by constants, or it goes to scratch memory)
-    c2_sync_n(pp.issued - pp.mark[o % kC2Ring]);
-    const u32x4* cb = pp.lds + (o % kC2Ring) * pp.WB;
-    u32x4* nb = pp.lds + ((o + LEAD) % kC2Ring) * pp.WB;
-    const int nmark = (o + LEAD) % kC2Ring;
+    // this tile's chunk c (DMA'd LEAD chunks back): every op of this wave younger than it may stay in
+    // flight.  Ring positions are static: every backward layer has 16 / CH chunks and starts at buffer 0
+    // (the mark array must only ever be indexed by constants, or it goes to scratch memory).  Pair mode:
+    // the wait and the weight DMA at the chunk's first tile only
+    const int c = o / CH;
+    const bool first = o % CH == 0;
+    if (first) c2_sync_n(pp.issued - pp.mark[c % kC2Ring]);
+    const u32x4* cb = pp.lds + (c % kC2Ring) * pp.WB + (o % CH) * TU;
+    u32x4* nb = pp.lds + ((c + LEAD) % kC2Ring) * pp.WB;
+    const int nmark = (c + LEAD) % kC2Ring;
     // the weight DMA of chunk o + LEAD (this layer's, or the next image's first tiles) in its loop form
     // (unrolled measured 149 -> 141 TFLOP/s), then this tile's h DMA and the dz store of tile o - 2
     // (h first: the counted wait of tile o + 1 retires only ops OLDER than chunk o + 1's weight DMA,
@@ -454,15 +466,18 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP],
         if (o + 2 < DT) dma16(rh, slots + ((o + 2) % SL) * 64, voff, 64 * (o + 2));
         else if (has_next_h) dma16(rh_next, slots + ((o + 2) % SL) * 64, voff, 64 * (o + 2 - DT));
       }
-      const int t = o + LEAD;
-      if (t < DT) {
-        dma_image(nb, Wt + (size_t)t * TU, TU, kC2Waves, pp.wave, pp.lane);
-        pp.issued += dma_image_count(TU, kC2Waves, pp.wave);
-      } else if (nextW && t - DT < next_tiles) {
-        dma_image(nb, nextW + (size_t)(t - DT) * next_n16, next_n16, kC2Waves, pp.wave, pp.lane);
-        pp.issued += dma_image_count(next_n16, kC2Waves, pp.wave);
+      if (first) {
+        const int t = c + LEAD;            // chunk to request
+        if (t < NC) {
+          dma_image(nb, Wt + (size_t)t * CH * TU, CH * TU, kC2Waves, pp.wave, pp.lane);
+          pp.issued += dma_image_count(CH * TU, kC2Waves, pp.wave);
+        } else if (nextW && (t - NC) * CH < next_tiles) {
+          const int nt = min(CH, next_tiles - (t - NC) * CH);
+          dma_image(nb, nextW + (size_t)(t - NC) * CH * next_n16, nt * next_n16, kC2Waves, pp.wave, pp.lane);
+          pp.issued += dma_image_count(nt * next_n16, kC2Waves, pp.wave);
+        }
+        pp.mark[nmark] = pp.issued;
       }
-      pp.mark[nmark] = pp.issued;
       if (o >= 2) stores(o - 2);
     };
     f32x4 acc;
@@ -541,11 +556,11 @@ __global__ void __launch_bounds__(64 * kC2Waves) GNOT_C2_WPE(B16) chain2_bwd_ker
       dma16(r, slots + 64, voff, 64);
       pp.issued += 2;
     }
-    constexpr int TU1 = c2_tile_u4(KBL, NP);
+    constexpr int C1 = c2b_ch<NP, B16>() * c2_tile_u4(KBL, NP);   // the last Linear's chunk
 #pragma unroll
     for (int t = 0; t < c2b_lead<NP>(); ++t) {
-      dma_image(c2lds + t * LD::WB, wt(nl - 1) + (size_t)t * TU1, TU1, kC2Waves, wave, lane);
-      pp.issued += dma_image_count(TU1, kC2Waves, wave);
+      dma_image(c2lds + t * LD::WB, wt(nl - 1) + (size_t)t * C1, C1, kC2Waves, wave, lane);
+      pp.issued += dma_image_count(C1, kC2Waves, wave);
       pp.mark[t] = pp.issued;
     }
   }
@@ -619,14 +634,19 @@ __global__ void __launch_bounds__(64 * kC2Waves) GNOT_C2_WPE(B16) chain2_bwd_ker
     float dx[KT0][4];
 #pragma unroll
     for (int o = 0; o < KT0; ++o) {
-      c2_sync_n(pp.issued - pp.mark[o % kC2Ring]);
-      const u32x4* cb = c2lds + (o % kC2Ring) * LD::WB;
-      if (o + c2b_lead<NP>() < KT0) {
-        dma_image(c2lds + ((o + c2b_lead<NP>()) % kC2Ring) * LD::WB, W0 + (size_t)(o + c2b_lead<NP>()) * TU0, TU0,
-                  kC2Waves, wave, lane);
-        pp.issued += dma_image_count(TU0, kC2Waves, wave);
+      constexpr int CH = c2b_ch<NP, B16>(), LEAD = c2b_lead<NP>();
+      const int c = o / CH;
+      if (o % CH == 0) {
+        c2_sync_n(pp.issued - pp.mark[c % kC2Ring]);
+        const int t = c + LEAD;
+        if (t * CH < KT0) {
+          const int nt = min(CH, KT0 - t * CH);
+          dma_image(c2lds + (t % kC2Ring) * LD::WB, W0 + (size_t)t * CH * TU0, nt * TU0, kC2Waves, wave, lane);
+          pp.issued += dma_image_count(nt * TU0, kC2Waves, wave);
+        }
+        pp.mark[t % kC2Ring] = pp.issued;
       }
-      pp.mark[(o + c2b_lead<NP>()) % kC2Ring] = pp.issued;
+      const u32x4* cb = c2lds + (c % kC2Ring) * LD::WB + (o % CH) * TU0;
       f32x4 acc = c2_tile<KB, false, NP>(cb, bp, f32x4{0.f, 0.f, 0.f, 0.f}, lane);
 #pragma unroll
       for (int r = 0; r < 4; ++r) dx[o][r] = acc[r];
