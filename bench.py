@@ -441,8 +441,10 @@ def main():
         else:
             pipe, pipe_peak = "bf16 MFMA, six per fp32 block product (bf16x6)", BF16_MFMA_PEAK_TFLOPS / 6
         traffic = None
-        if not args.points and dtype == "fp32":
-            traffic = pmc_traffic(args.workload, rk, M["klaunch_step"])
+        if not args.points:
+            # entries: "<workload>/<class>" (fp32), "<workload>/bf16/<class>" (bf16 mode)
+            traffic = pmc_traffic(args.workload if dtype == "fp32" else f"{args.workload}/bf16", rk,
+                                  M["klaunch_step"])
         if rk == "wgrad_b16":
             # HBM-bound: every job is a 256 x 256 Linear reading (out + in) * 2 B of bf16 rows per point for
             # 2 * out * in flops, so algorithmic bytes = flops / 128
@@ -451,7 +453,7 @@ def main():
                 "kernel": names[rk], "class": rk,
                 "class_ms_per_step": {k: round(v[0], 3) for k, v in M["kinds"].items()},
                 "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "tflops": round(ach, 3), "frac_mfma": round(ach / BF16_MFMA_PEAK_TFLOPS, 4),
                 "avg_launch_us": round(avg_ms * 1e3, 2), "bytes_per_launch": flops_launch / 128.0,
                 "flops_per_launch": flops_launch, "launches": M["klaunch"],
@@ -469,6 +471,10 @@ def main():
             "pipe_peak": round(pipe_peak, 2),
             "frac_pipe": round(ach / pipe_peak, 4),
             "traffic": traffic,
+            # the measured HBM bytes per launch (PMC) over the live launch time: how far the class is from
+            # the memory side of its roofline (the one-piece bf16 chains are nearer to it than to the MFMA's)
+            "traffic_gbs": round(traffic / (avg_ms * 1e-3) / 1e9, 1) if traffic and avg_ms > 0 else None,
+            "traffic_frac_hbm": round(traffic / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if traffic and avg_ms > 0 else None,
             "avg_launch_us": round(avg_ms * 1e3, 2),
             "flops_per_launch": flops_launch,
             "launches": M["klaunch"],
