@@ -383,7 +383,7 @@ __global__ void __launch_bounds__(64 * kC2Waves) GNOT_C2_WPE(B16) chain2_fwd_ker
 // One backward layer l: g = W_l^T dz_l (DT output tiles of the split input `in`), dz_{l-1} = g *
 // gelu'(h_{l-1}) stored (rz) and kept in nx.  Weight chunks stream through the ring c2b_lead<NP>() tiles
 // ahead (the last tiles request the next image's first chunks); each tile's wait retires its own chunk
-// and leaves every younger op of the wave in flight (C2Pipe::younger).  The saved pre-activation tiles
+// and leaves every younger op of the wave in flight (C2Pipe::issued / mark).  The saved pre-activation tiles
 // h_{l-1} arrive by LDS-DMA two tiles ahead into this wave's slots (tile o in slot o % kSlots; the next
 // layer's tiles 0 and 1 are requested by this layer's last two tiles).  Entry: the layer's first
 // c2b_lead<NP>() chunks and its h tiles 0 and 1 requested.
@@ -535,7 +535,6 @@ __global__ void __launch_bounds__(64 * kC2Waves) GNOT_C2_WPE(B16) chain2_bwd_ker
   float* dz = a.dz + e * a.dz_chain_stride;
   if (WALK && e > e_begin) {
     __syncthreads();            // every wave is done with the previous expert's chunks and slots
-    pp.cnt = 0;
   }
   auto wt = [&](int l) { return reinterpret_cast<const u32x4*>(L[l].WpT); };
   const unsigned lb = B16 ? lay_b16 : lay_bytes;

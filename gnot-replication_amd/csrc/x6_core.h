@@ -171,9 +171,10 @@ GNOT_DEV void c2_sync_n(int n) {   // n is wave-uniform and small
   }
 }
 // the weight-chunk stream of a chain kernel (chain2.hip): a ring of kC2Ring chunk buffers.  The
-// forward keeps one chunk in flight (nxt); the backward keeps GNOT_C2B_LEAD in flight and waits for a
-// chunk with a counted vmcnt: `issued` counts this wave's vector-memory ops as they are issued, mark[b] is
-// that count right after the DMA of the chunk in buffer b, so issued - mark[b] ops are younger than it
+// forward keeps one chunk in flight (cur / nxt by the chunk count cnt); the backward keeps
+// c2b_lead<NP>() in flight at static ring positions and waits for a chunk with a counted vmcnt: `issued`
+// counts this wave's vector-memory ops as they are issued, mark[b] is that count right after the DMA of
+// the chunk in buffer b, so issued - mark[b] ops are younger than it
 constexpr int kC2Ring = 4;
 struct C2Pipe {
   u32x4* lds;
@@ -184,9 +185,6 @@ struct C2Pipe {
   int mark[kC2Ring] = {0, 0, 0, 0};
   GNOT_DEV const u32x4* cur() const { return lds + (cnt % kC2Ring) * WB; }
   GNOT_DEV u32x4* nxt() const { return lds + ((cnt + 1) % kC2Ring) * WB; }
-  GNOT_DEV u32x4* at(int k) const { return lds + ((cnt + k) % kC2Ring) * WB; }
-  // vector-memory ops younger than the DMA of the chunk about to be consumed
-  GNOT_DEV int younger() const { return issued - mark[cnt % kC2Ring]; }
 };
 // this wave's instruction count of dma_image(lds, src, n16, nwaves, wave, lane)
 GNOT_DEV int dma_image_count(int n16, int nwaves, int wave) {
