@@ -238,13 +238,19 @@ __global__ void __launch_bounds__(64 * kC2Waves) GNOT_C2_WPE(B16) chain2_fwd_ker
   const long p = ((long)blockIdx.x * kC2Waves + wave) * 16 + (lane & 15);
   const bool valid = p < a.P;
   const int nl = a.nlin;
-  const unsigned lay_bytes = (unsigned)min((long)a.P * D * 4, 0xFFFFFFFFL);   // one [P, D] layer
-  // byte offset of this lane's row in a [P, D] layer: unsigned (the plan bounds P * D * 4 < 2^32)
-  const int voff = (int)(((unsigned)(blockIdx.x * kC2Waves + wave) * 16u + (unsigned)(lane & 15)) * (unsigned)(D * 4) +
-                         16u * (unsigned)g);
-  // B16: this lane's row in the bf16 layers (512 B per point; the plan bounds P * 512 < 2^32)
-  const int rowb = (int)(((unsigned)(blockIdx.x * kC2Waves + wave) * 16u + (unsigned)(lane & 15)) * (unsigned)kB16Row);
-  const unsigned lay_b16 = (unsigned)min((long)a.P * kB16Row, 0xFFFFFFFFL);
+  // Every buffer resource of a layer starts at this workgroup's first row (64-bit base in SGPRs), so the
+  // 32-bit offsets only span the workgroup's 128 rows: no bound on the point count of a launch.  Rows
+  // past P read 0 / are dropped by the resource's bound (the workgroup's rows that exist).
+  const long row0 = (long)blockIdx.x * kC2Waves * 16;
+  const int nrows = (int)min((long)kC2Waves * 16, (long)a.P - row0);
+  const unsigned lay_bytes = (unsigned)nrows * (unsigned)(D * 4);   // this workgroup's rows of a [P, D] layer
+  // byte offset of this lane's row within the workgroup's rows
+  const int voff = (int)(((unsigned)wave * 16u + (unsigned)(lane & 15)) * (unsigned)(D * 4) + 16u * (unsigned)g);
+  // B16: this lane's row in the bf16 layers (512 B per point)
+  const int rowb = (int)(((unsigned)wave * 16u + (unsigned)(lane & 15)) * (unsigned)kB16Row);
+  const unsigned lay_b16 = (unsigned)nrows * (unsigned)kB16Row;
+  // float offset of the workgroup's first row in a layer (fp32: D floats per row; B16: 512 B = 128 floats)
+  const long rbase = row0 * (B16 ? kB16Row / 4 : D);
   C2Pipe pp{c2lds, LD::WB, 0, wave, lane};
   constexpr int CH = c2f_pair<NP>() ? 2 : 1;         // output tiles per weight chunk
   // a layer's first wait: the saves the previous layer issued after its last weight DMA (its last
@@ -263,12 +269,12 @@ __global__ void __launch_bounds__(64 * kC2Waves) GNOT_C2_WPE(B16) chain2_fwd_ker
   dma_image(c2lds, W0, CH * c2_tile_u4(KB0, NP), kC2Waves, wave, lane);
   auto wp = [&](int l) { return reinterpret_cast<const u32x4*>(L[l].Wp); };
   auto rs = [&](int l) {
-    return make_rsrc(SAVE ? save + l * a.save_layer_stride : nullptr, SAVE ? (B16 ? lay_b16 : lay_bytes) : 0u);
+    return make_rsrc(SAVE ? save + l * a.save_layer_stride + rbase : nullptr, SAVE ? (B16 ? lay_b16 : lay_bytes) : 0u);
   };
   const int svoff = B16 ? rowb : voff;
   // B16: a Linear's bf16 input words (k-blocks 0 .. nkb-1) into save slot `slot`; returns the stores issued
   auto store_in = [&](const float* slot, const u32x4 (&w)[KB][NP], int nkb) __attribute__((always_inline)) {
-    const rsrc_t r = make_rsrc(slot, lay_b16);
+    const rsrc_t r = make_rsrc(slot + rbase, lay_b16);
 #pragma unroll
     for (int t = 0; t < KB; ++t)
       if (t < nkb) buf_store_b128(w[t][0], r, rowb + (t * 4 + g) * 16);
@@ -519,13 +525,15 @@ __global__ void __launch_bounds__(64 * kC2Waves) GNOT_C2_WPE(B16) chain2_bwd_ker
   const long p = ((long)blockIdx.x * kC2Waves + wave) * 16 + (lane & 15);
   const bool valid = p < a.P;
   const int nl = a.nlin;
-  const unsigned lay_bytes = (unsigned)min((long)a.P * D * 4, 0xFFFFFFFFL);   // one [P, D] layer
-  // byte offset of this lane's row in a [P, D] layer: unsigned (the plan bounds P * D * 4 < 2^32)
-  const int voff = (int)(((unsigned)(blockIdx.x * kC2Waves + wave) * 16u + (unsigned)(lane & 15)) * (unsigned)(D * 4) +
-                         16u * (unsigned)g);
+  // buffer resources start at this workgroup's first row (chain2_fwd_kernel): 32-bit offsets span 128 rows
+  const long row0 = (long)blockIdx.x * kC2Waves * 16;
+  const int nrows = (int)min((long)kC2Waves * 16, (long)a.P - row0);
+  const unsigned lay_bytes = (unsigned)nrows * (unsigned)(D * 4);
+  const int voff = (int)(((unsigned)wave * 16u + (unsigned)(lane & 15)) * (unsigned)(D * 4) + 16u * (unsigned)g);
   // B16: this lane's row in the bf16 layers (512 B per point)
-  const int rowb = (int)(((unsigned)(blockIdx.x * kC2Waves + wave) * 16u + (unsigned)(lane & 15)) * (unsigned)kB16Row);
-  const unsigned lay_b16 = (unsigned)min((long)a.P * kB16Row, 0xFFFFFFFFL);
+  const int rowb = (int)(((unsigned)wave * 16u + (unsigned)(lane & 15)) * (unsigned)kB16Row);
+  const unsigned lay_b16 = (unsigned)nrows * (unsigned)kB16Row;
+  const long rbase = row0 * (B16 ? kB16Row / 4 : D);
   const int lvoff = B16 ? rowb : voff;               // what the layers address rows with
   C2Pipe pp{c2lds, LD::WB, 0, wave, lane};
   constexpr int e_begin = 0;
@@ -538,8 +546,8 @@ __global__ void __launch_bounds__(64 * kC2Waves) GNOT_C2_WPE(B16) chain2_bwd_ker
   }
   auto wt = [&](int l) { return reinterpret_cast<const u32x4*>(L[l].WpT); };
   const unsigned lb = B16 ? lay_b16 : lay_bytes;
-  auto rh = [&](int l) { return make_rsrc(save + l * a.save_layer_stride, lb); };   // h_l
-  auto rz = [&](int l) { return make_rsrc(dz + l * a.dz_layer_stride, lb); };      // dz_l
+  auto rh = [&](int l) { return make_rsrc(save + l * a.save_layer_stride + rbase, lb); };   // h_l
+  auto rz = [&](int l) { return make_rsrc(dz + l * a.dz_layer_stride + rbase, lb); };      // dz_l
   // prologue DMA: the last Linear's first c2b_lead<NP>() weight chunks (ring buffers 0 ..) and the first
   // two h_{nl-2} tiles (B16: pairs 0 .. GNOT_C2B_K - 1)
   // (h first: a chunk's counted wait retires only the ops older than its DMA)

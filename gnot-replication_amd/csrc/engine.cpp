@@ -29,9 +29,6 @@ static int fail(int code, const std::string& msg) {
   return code;
 }
 
-// rows of one plan: a [rows, 3d] fp32 array must stay addressable by a 32-bit buffer byte offset
-static long max_rows_per_plan(int D) { return 0xFFFFFFFFL / (12L * D); }
-
 #define GNOT_CK(expr)                                                                           \
   do {                                                                                          \
     hipError_t e_ = (expr);                                                                     \
@@ -174,6 +171,7 @@ struct gnot_plan {
   bool ws_bound = false;
   bool packed = false;
   bool fwd_done = false;
+  bool bwd_done = false;      // a gnot_backward ran after the last gnot_forward (gnot_input_grads needs it)
 
   // point sharding (gnot_plan_set_shard): sample b's points are split over `world` ranks
   int world = 1, rank = 0;
@@ -284,6 +282,13 @@ extern "C" int gnot_plan_create(const gnot_config* cfg, gnot_plan** out) {
     return fail(GNOT_E_INVALID, "hidden width must be a multiple of 16 up to 192, or 256, on the MI355X kernels");
   if (dh % 4 != 0 || dh > 64)
     return fail(GNOT_E_INVALID, "head width d/n_head must be a multiple of 4 up to 64 on the MI355X kernels");
+  // the projections' fused feature softmax needs whole heads per workgroup: linear2.hip (d = 256) takes
+  // dh = 16 / 32 / 64; linear.hip (the d <= 192 projections and the batched input-function K/V at any d)
+  // a tiling of whole heads (linear_oc)
+  if (D == 256 && dh != 16 && dh != 32 && dh != 64)
+    return fail(GNOT_E_INVALID, "at hidden width 256 the head width must be 16, 32 or 64 on the MI355X kernels");
+  if ((D != 256 && (linear_oc(D, 3 * D, 2 * D, dh) < 0 || linear_oc(D, D, D, dh) < 0)) || linear_oc(D, 2 * D, 1, dh) < 0)
+    return fail(GNOT_E_INVALID, "no projection tiling keeps whole heads of this head width on the MI355X kernels");
   if (c.n_expert < 1 || c.n_attn_layers < 0 || c.n_input_functions < 0 || c.n_input_functions > 8)
     return fail(GNOT_E_INVALID, "bad n_expert / n_attn_layers / n_input_functions");
   if (c.input_dim + c.theta_dim > D || c.input_dim > D || c.input_func_dim > D || c.out_dim > D ||
@@ -568,6 +573,11 @@ static void finish_group(gnot_plan* p, WgradGroup& G) {
     const long minpts = kMinSplitPoints;   // >= 4 LDS stages per workgroup: bounds the split-K slab traffic
     const long maxs = std::max<long>(1, (J.P + minpts - 1) / minpts);
     J.splits = (int)std::min<long>(std::min<long>(want, maxs), 256);
+    // the wide / bf16-row kernels address one split through a buffer resource based at its first row
+    // with 32-bit offsets: a split's rows (+ the stage loaded past its end) stay below 2^31 bytes
+    const long row_bytes = G.b16 ? 512L : 4L * std::max<long>(std::max<long>(J.lddz, J.ldx), 1);
+    const long max_pts = ((1L << 31) - 1) / row_bytes - 64;
+    J.splits = (int)std::max<long>(J.splits, (J.P + max_pts - 1) / max_pts);
     const int nt = J.diag_only ? J.tiles_o : J.tiles_o * J.tiles_i;
     J.slab_off = (long)G.slab_floats;
     G.slab_floats += (size_t)J.splits * nt * kPTile * (kPTile + 1);
@@ -1033,18 +1043,11 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
     p->Q[i] = p->fnoff[i][B];
   }
   if (p->P <= 0) return fail(GNOT_E_INVALID, "empty batch (no query points)");
+  // point / chunk indices are 32-bit in the kernels' job tables (the buffer resources of the streaming
+  // kernels are based per workgroup or per split, so no activation array size bounds a plan)
   if (p->P >= (1L << 31) / 4) return fail(GNOT_E_INVALID, "batch too large for 32-bit segment indices");
-  // the kernels address one activation array through a buffer resource with a 32-bit byte offset;
-  // the widest is a [rows, 3d] q|k|v projection (d = 256: at most 1,398,101 points per GPU)
-  {
-    const long lim = max_rows_per_plan(p->D);
-    if (p->P > lim) return fail(GNOT_E_INVALID, "more than " + std::to_string(lim) +
-                                                    " query points on one GPU (32-bit activation offsets at this width); "
-                                                    "point-shard the mesh (gnot_plan_set_shard)");
-    for (int i = 0; i < p->I; ++i)
-      if (p->Q[i] > lim)
-        return fail(GNOT_E_INVALID, "more than " + std::to_string(lim) + " input-function points on one GPU");
-  }
+  for (int i = 0; i < p->I; ++i)
+    if (p->Q[i] >= (1L << 31) / 4) return fail(GNOT_E_INVALID, "input functions too large for 32-bit segment indices");
   p->training = training != 0;
   p->sharded = p->world > 1;
   if (p->input_grads && p->sharded)
@@ -1396,6 +1399,7 @@ extern "C" int gnot_plan_bind_workspace_async(gnot_plan* p, void* workspace, siz
   p->ws_bound = true;
   p->packed = false;
   p->fwd_done = false;
+  p->bwd_done = false;
   return GNOT_OK;
 }
 
@@ -1811,6 +1815,7 @@ extern "C" int gnot_forward(gnot_plan* p, const float* x, const float* theta, co
     GNOT_CK(launch_chain_fwd(a, c.s));
   }
   p->fwd_done = true;
+  p->bwd_done = false;
   return GNOT_OK;
 }
 
@@ -1962,6 +1967,7 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
   GNOT_CK(hipEventRecord(join, p->side));
   GNOT_CK(hipStreamWaitEvent(c.s, join, 0));
   p->readers.clear();
+  p->bwd_done = true;
   return GNOT_OK;
 }
 
@@ -1970,6 +1976,9 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
 extern "C" int gnot_input_grads(gnot_plan* p, float* dx, float* dtheta, float* const* dfns, void* stream) {
   if (!p || !p->input_grads || !p->ws_bound || !p->training)
     return fail(GNOT_E_STATE, "gnot_plan_set_input_grads(plan, 1) and a training batch are required");
+  if (!p->bwd_done)
+    return fail(GNOT_E_STATE, "gnot_input_grads reads the encoders' input gradients of a gnot_backward, which must "
+                              "follow the last gnot_forward");
   const hipStream_t s = static_cast<hipStream_t>(stream);
   const Buf& xin = p->bufs.at("dxin");
   const Buf& xg = p->bufs.at("dxg");

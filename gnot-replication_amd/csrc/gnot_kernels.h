@@ -53,6 +53,9 @@ struct LinearArgs {
   int np = 3;                        // linear2: operand pieces (3 = bf16x6, 1 = bf16 mode)
 };
 hipError_t launch_linear(const LinearArgs& a, int D, hipStream_t s);
+// output tiles per workgroup of linear.hip for an NO-column projection with a softmax epilogue over its
+// first nsoft columns in heads of dh (-1: no tiling keeps whole heads per workgroup)
+int linear_oc(int D, int NO, int nsoft, int dh);
 // d = 256 projections on bf16x6 MFMA (linear2.hip): Wp[s] are OUTPUT-MAJOR x6 images (pack x6 = 2)
 bool linear2_supported(const LinearArgs& a, int D);
 hipError_t launch_linear2(const LinearArgs& a, hipStream_t s);

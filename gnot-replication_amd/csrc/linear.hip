@@ -93,32 +93,37 @@ __global__ void __launch_bounds__(256) linear_batch_kernel(const LinearArgs* __r
 // projection is ~1,250 waves at 4 tiles, 2,500 at 2), but the input rows are re-read once per chunk
 // and the extra waves compete with the side-stream weight-gradient GEMMs: measured at cfg2, 4 tiles
 // 3.57 ms/step, 8 tiles 3.74, 2 tiles 3.75, 1 tile 4.00.
-// GNOT_LINEAR_OC overrides the choice (experiments); a choice that does not tile D and NO, or whose
-// chunks would split a softmax head (16 * oc not a multiple of dh), falls back to the widest valid one.
-static int linear_oc(int D, int NO, int nsoft, int dh) {
+// Chunks of a softmax epilogue must hold whole heads (16 * oc a multiple of dh): oc = D / 16 (the whole
+// row) always does, so every (D, dh) the plan accepts has a valid choice (e.g. d = 144 with 4 heads of
+// 36: the divisors 1 and 3 of 9 tiles split a head, 9 does not).  GNOT_LINEAR_OC overrides the choice
+// (experiments); a choice that does not tile D and NO, or would split a head, falls back to the widest
+// valid one; -1 when none exists (the launch then fails instead of skipping the softmax).
+int linear_oc(int D, int NO, int nsoft, int dh) {
   static const int env = [] {
     const char* e = getenv("GNOT_LINEAR_OC");
     return e ? atoi(e) : 0;
   }();
   const int kt = D / 16;
   auto ok = [&](int oc) {
-    return oc >= 1 && oc <= 8 && kt % oc == 0 && NO % (16 * oc) == 0 && (nsoft == 0 || (16 * oc) % dh == 0);
+    return oc >= 1 && (oc <= 8 || oc == kt) && kt % oc == 0 && NO % (16 * oc) == 0 &&
+           (nsoft == 0 || (16 * oc) % dh == 0);
   };
   int want = env > 0 ? env : 4;
   if (ok(want)) return want;
-  for (int oc = 8; oc >= 1; --oc)
+  for (int oc = kt; oc >= 1; --oc)
     if (ok(oc)) return oc;
-  return 1;
+  return -1;
 }
 
-// every (D, oc) linear_oc can return: oc a divisor of D / 16 (<= 8)
+// every (D, oc) linear_oc can return: oc a divisor of D / 16 (<= 8, or D / 16 itself)
 #define GNOT_LIN_CASES                                                                                  \
   GNOT_LIN(16, 1) GNOT_LIN(32, 1) GNOT_LIN(32, 2) GNOT_LIN(48, 1) GNOT_LIN(48, 3) GNOT_LIN(64, 1)         \
   GNOT_LIN(64, 2) GNOT_LIN(64, 4) GNOT_LIN(80, 1) GNOT_LIN(80, 5) GNOT_LIN(96, 1) GNOT_LIN(96, 2)         \
   GNOT_LIN(96, 3) GNOT_LIN(96, 6) GNOT_LIN(112, 1) GNOT_LIN(112, 7) GNOT_LIN(128, 1) GNOT_LIN(128, 2)     \
-  GNOT_LIN(128, 4) GNOT_LIN(128, 8) GNOT_LIN(144, 1) GNOT_LIN(144, 3) GNOT_LIN(160, 1) GNOT_LIN(160, 2)   \
-  GNOT_LIN(160, 5) GNOT_LIN(176, 1) GNOT_LIN(192, 1) GNOT_LIN(192, 2) GNOT_LIN(192, 3) GNOT_LIN(192, 4)   \
-  GNOT_LIN(192, 6) GNOT_LIN(256, 1) GNOT_LIN(256, 2) GNOT_LIN(256, 4) GNOT_LIN(256, 8)
+  GNOT_LIN(128, 4) GNOT_LIN(128, 8) GNOT_LIN(144, 1) GNOT_LIN(144, 3) GNOT_LIN(144, 9) GNOT_LIN(160, 1)   \
+  GNOT_LIN(160, 2) GNOT_LIN(160, 5) GNOT_LIN(160, 10) GNOT_LIN(176, 1) GNOT_LIN(176, 11) GNOT_LIN(192, 1) \
+  GNOT_LIN(192, 2) GNOT_LIN(192, 3) GNOT_LIN(192, 4) GNOT_LIN(192, 6) GNOT_LIN(192, 12) GNOT_LIN(256, 1)  \
+  GNOT_LIN(256, 2) GNOT_LIN(256, 4) GNOT_LIN(256, 8)
 
 hipError_t launch_linear(const LinearArgs& a, int D, hipStream_t s) {
   if (a.P <= 0) return hipSuccess;

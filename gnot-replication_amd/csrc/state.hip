@@ -28,10 +28,10 @@ GNOT_DEV int find_job_s(const int* __restrict__ prefix, int njobs, int idx) {
   return lo;
 }
 
-constexpr int kMaxBlk = 4;
+constexpr int kMaxBlk = 4;   // 4x4 output blocks per thread: H*(dh/4)^2 <= 1024 (d <= 256, dh <= 64)
 // floats of one row-stage region: pts * d rounded up to whole 64-lane x 16-byte DMA instructions
 // (d > 128 takes pts = 8192 / d, e.g. 56 points x 144 = 8,064 floats: 31.5 instructions)
-__host__ __device__ constexpr int state_stage_floats(int pts, int d) { return (pts * d + 255) / 256 * 256; }   // 4x4 output blocks per thread: H*(dh/4)^2 <= 1024 (d <= 256, dh <= 64)
+__host__ __device__ constexpr int state_stage_floats(int pts, int d) { return (pts * d + 255) / 256 * 256; }
 
 // One workgroup = state_pts(d) points of one job.  The workgroup first pulls all of its A and B
 // rows into LDS with LDS-DMA (global_load_lds, 16 B per lane, every load in flight at once: one

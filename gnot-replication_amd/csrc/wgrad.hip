@@ -431,14 +431,17 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
   struct Raw {
     float a[8], b[8];
   };
-  // buffer loads: rows past the job's P read 0 (only the last split ends inside a stage: chunks are
-  // whole stages), columns past out / in are masked; the row offset is wave-uniform (SGPR)
-  const rsrc_t rA = make_rsrc(J.dz, (unsigned)min((long)J.P * J.lddz * 4, 0xFFFFFFFFL));
-  const rsrc_t rB = make_rsrc(J.x, (unsigned)min((long)J.P * J.ldx * 4, 0xFFFFFFFFL));
+  // buffer loads from resources based at the split's first row (64-bit base, so the 32-bit offsets span
+  // one split: finish_group bounds a split's rows x pitch below 2^31 bytes): rows past the split read 0
+  // (only the last split ends inside a stage: chunks are whole stages; the loads one stage past a split's
+  // end are never staged), columns past out / in are masked; the row offset is wave-uniform (SGPR)
+  const long nsp = pe > pb ? pe - pb : 0;
+  const rsrc_t rA = make_rsrc(J.dz + pb * J.lddz, (unsigned)(nsp * J.lddz * 4));
+  const rsrc_t rB = make_rsrc(J.x + pb * J.ldx, (unsigned)(nsp * J.ldx * 4));
   const int voA = fca * 4, voB = fcb * 4;
   const int hw = __builtin_amdgcn_readfirstlane(hh);
   auto load = [&](Raw& R, long p0) {
-    const unsigned pr = (unsigned)(p0 + 8 * hw);
+    const unsigned pr = (unsigned)(p0 - pb + 8 * hw);
     // raw values only: any arithmetic on them here would make the wave wait for the load now
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -542,7 +545,7 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
 #pragma unroll
         for (int q = 0; q < NP; ++q) af[0][q] = A[q * kWPiece + (wr * 4) * 64 + lane];
         float ra[8], vb[8];
-        const unsigned pr = (unsigned)(pn + 8 * hw);
+        const unsigned pr = (unsigned)(pn - pb + 8 * hw);
         auto chunk = [&](int k) {
           ra[k] = (!decltype(MASK)::value || fa) ? R.a[k] : 0.f;
           dbacc += ra[k];
@@ -723,15 +726,17 @@ __global__ void __launch_bounds__(kWThreads) pgemm_b16_kernel(const WgradJob* __
   const long pe = min((long)J.P, pb + chunk);
   const int nst = pe > pb ? (int)((pe - pb + kBStage - 1) / kBStage) : 0;
   const int wr = wave >> 2, wc = wave & 3;
-  // rows past the job's P read 0 (only the last split's last stage reaches past it)
-  const unsigned bytes = (unsigned)min((long)J.P * kB16Row, 0xFFFFFFFFL);
-  const rsrc_t rA = make_rsrc(J.dz, bytes), rB = make_rsrc(J.x, bytes);
+  // resources based at the split's first row: rows past the split read 0 (only the last split's last
+  // stage reaches past it)
+  const unsigned bytes = (unsigned)((pe > pb ? pe - pb : 0) * kB16Row);
+  const long rb = pb * (kB16Row / 4);                        // the split's first row, in 4-byte units
+  const rsrc_t rA = make_rsrc(J.dz + rb, bytes), rB = make_rsrc(J.x + rb, bytes);
   // DMA role: wave w brings rows 2w, 2w+1 (instruction 0) and 2w+16, 2w+17 (instruction 1) of both
   // operands; (r & 3) is the same for both instructions
   const int hi = lane >> 5;
   const int dvoff = hi * kB16Row + (((lane & 31) ^ (((2 * wave + hi) & 3) << 2)) * 16);
   auto dma_stage = [&](int s) __attribute__((always_inline)) {
-    const unsigned p0 = (unsigned)(pb + (long)s * kBStage);
+    const unsigned p0 = (unsigned)(s * kBStage);           // relative to the split's first row
     u32x4* slot = bl + (s % kBSlots) * (kBSlotBytes / 16);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {

@@ -73,9 +73,10 @@ int gnot_plan_bind_params(gnot_plan* plan, const float* const* weights, const fl
  * x_off[b] .. x_off[b+1]-1); fn_off: host array [n_input_functions * (B+1)] of the same for every
  * input function.  A zero-padded batch (main.py:60-82) is simply x_off = {0, N, 2N, ...}.
  * training != 0 keeps the activations the backward needs.
- * Limits: at most 0xFFFFFFFF / (12 d) points per plan (query points, and points of each input
- * function): the kernels address a [rows, 3d] fp32 activation through a 32-bit buffer byte offset
- * (d = 256: 1,398,101 points per GPU; point-shard larger meshes).  GNOT_E_INVALID beyond it. */
+ * Limits: fewer than 2^29 points per plan (query points, and points of each input function: the
+ * kernels' job tables hold 32-bit point indices; their buffer resources are based per workgroup or per
+ * split-K range, so no activation array size bounds a plan).  GNOT_E_INVALID beyond it; the real bound
+ * is the workspace (gnot_plan_workspace_bytes) against the device memory. */
 int gnot_plan_set_batch(gnot_plan* plan, int B, const int64_t* x_off, const int64_t* fn_off, int training);
 
 /* MoE activation recompute (off by default): training keeps only each MoE call's input and the

@@ -48,9 +48,12 @@ def _case(cfg, Ns, Ms, seed):
     return fx
 
 
-def _rank(rank, world, port, cfg, Ns, Ms, q, backend="gloo"):
+def _rank(rank, world, port, cfg, Ns, Ms, q, backend="gloo", fx=None, env=None):
+    """One rank: its slice of every sample through the sharded engine; rank 0 gathers and checks.  `fx`
+    (with fx["G"]): a precomputed case (else _case(cfg, Ns, Ms)); `env`: environment for the rank."""
     sys.path[:0] = [ROOT, os.path.join(ROOT, "gnot-replication_amd"), os.path.join(ROOT, "tests")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(env or {})
     if backend == "nccl":
         torch.cuda.set_device(0)
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
@@ -60,7 +63,8 @@ def _rank(rank, world, port, cfg, Ns, Ms, q, backend="gloo"):
         from golden_util import check_parity, model_args
         from gnot_amd import GNOT
         from gnot_amd import parallel as par
-        fx = _case(cfg, Ns, Ms, seed=11)
+        if fx is None:
+            fx = _case(cfg, Ns, Ms, seed=11)
         dev = torch.device("cuda", 0)
         m = GNOT(*model_args(cfg)).to(dev)
         m.load_state_dict({k: torch.from_numpy(v).float() for k, v in fx["params"].items()})
@@ -136,4 +140,32 @@ def test_point_sharded_gnot_rccl_path():
     errs = q.get(timeout=100)
     p.join(timeout=30)
     assert p.exitcode == 0, p.exitcode
+    assert not errs, errs
+
+
+@pytest.mark.timeout(600)
+def test_point_sharded_configs3_widths_70k_points(mid_case):
+    """configs[3]'s model widths (d=256, 8 heads, 8 experts, 4-layer MLPs, one 805-point input function;
+    L = 1 block) on one 70,000-point mesh split over 2 ranks (35,000 points each, gloo host staging on one
+    GPU) vs the float64 oracle at 1e-4: the sharded run takes the kernels a 1M / 8 rank does -- the MFMA
+    attention apply / K-V backward (>= 8,192 points), the MFMA state partials (GNOT_STATE_MFMA_MIN=16384
+    in the ranks: per-rank groups of 35,000 points), the wide weight gradients -- and real exchange
+    tables (the scramble of 8 heads over 70,000 points is 16 runs per rank pair).  Anchor: the all-point
+    state sums model.py:98-100 (all-reduced) and the head-major reshape model.py:103-104 (all-to-all)."""
+    fx, G = mid_case
+    fx = dict(fx, G=G)
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    env = {"GNOT_STATE_MFMA_MIN": "16384"}
+    procs = [ctx.Process(target=_rank, args=(r, world, port, fx["cfg"], [int(fx["x_off"][-1])], [[805]], q),
+                         kwargs=dict(fx=fx, env=env))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    errs = q.get(timeout=400)
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert not errs, errs

@@ -31,6 +31,8 @@ CASES = {
     "d96_h8": _cfg(96, 8, 3, 1),          # dh 12: heads straddle 16-feature tiles
     "d112_h4": _cfg(112, 4, 2, 2),        # dh 28, two input functions
     "d144_h3": _cfg(144, 3, 2, 1),        # dh 48 above d = 128
+    "d144_h4": _cfg(144, 4, 2, 1),        # dh 36: only the whole 9-tile row keeps a head in one projection workgroup
+    "d176_h4": _cfg(176, 4, 2, 0),        # dh 44: 11 tiles, self-attention (fused q|k|v softmax) only
     "d160_h8": _cfg(160, 8, 2, 1),        # dh 20
     "d192_h8": _cfg(192, 8, 2, 0),        # dh 24, self-attention only
     "d192_h6": _cfg(192, 6, 2, 1, nl=4),  # dh 32 (fp32-MFMA attention forms at d = 192)

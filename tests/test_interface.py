@@ -110,9 +110,11 @@ def test_plan_rejects_bad_config_and_batch():
         lib.gnot_plan_destroy(plan)
 
 
-def test_plan_rejects_meshes_past_the_32bit_offset_limit():
-    """gnot_plan_set_batch bounds the points per plan so every [rows, 3d] activation stays addressable
-    by the kernels' 32-bit buffer offsets (gnot_hip.h: 0xFFFFFFFF / (12 d); d = 256 -> 1,398,101)."""
+def test_plan_accepts_meshes_past_the_old_32bit_offset_limit():
+    """The streaming kernels base their buffer resources per workgroup / per split-K range (64-bit base,
+    32-bit in-tile offsets), so a plan takes configs[4]'s ~1.6M points and configs[3]'s 1M-point mesh at
+    d = 256 on one GPU (round 3 refused more than 0xFFFFFFFF / (12 d) = 1,398,101 points).  Only the
+    32-bit point indices of the job tables bound a plan (2^29 points)."""
     from gnot_amd import _lib
     lib = _lib.load()
     cfg = _lib.GnotConfig(input_dim=3, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=1,
@@ -121,14 +123,14 @@ def test_plan_rejects_meshes_past_the_32bit_offset_limit():
     plan = ctypes.c_void_p()
     _lib.check(lib.gnot_plan_create(ctypes.byref(cfg), ctypes.byref(plan)))
     try:
-        lim = 0xFFFFFFFF // (12 * 256)
-        assert lim == 1398101
         fo = (ctypes.c_int64 * 2)(0, 805)
-        _lib.check(lib.gnot_plan_set_batch(plan, 1, (ctypes.c_int64 * 2)(0, lim), fo, 0))
-        assert lib.gnot_plan_set_batch(plan, 1, (ctypes.c_int64 * 2)(0, lim + 1), fo, 0) == -1
-        assert b"point-shard" in lib.gnot_last_error()
+        for n in (1398102, 4_000_000):
+            _lib.check(lib.gnot_plan_set_batch(plan, 1, (ctypes.c_int64 * 2)(0, n), fo, 1))
+            assert lib.gnot_plan_workspace_bytes(plan) > n * 256 * 4
+        assert lib.gnot_plan_set_batch(plan, 1, (ctypes.c_int64 * 2)(0, 1 << 29), fo, 0) == -1
+        assert b"32-bit" in lib.gnot_last_error()
         assert lib.gnot_plan_set_batch(plan, 1, (ctypes.c_int64 * 2)(0, 1000),
-                                       (ctypes.c_int64 * 2)(0, lim + 1), 0) == -1
+                                       (ctypes.c_int64 * 2)(0, 1 << 29), 0) == -1
     finally:
         lib.gnot_plan_destroy(plan)
 
