@@ -1,7 +1,7 @@
 // Attention apply passes on fp32 MFMA (v_mfma_f32_16x16x4_f32: exact fp32 products, fp32 sums) --
 // the Q . state contractions of reference LinearAttention.forward (model.py:78-80 / 99-101) and their
 // backward, for head widths dh = 16, 32, 64.  Same arguments and results as attn.hip's VALU kernels
-// (which stay for other head widths and as the A/B reference, env GNOT_APPLY_VALU).
+// (which stay for other head widths and for small meshes, GNOT_APPLY_MFMA_MIN).
 //
 // Point form (gnot_common.h): a wave owns 16 points; lane l holds, for every 16-feature tile T of a
 // head, features 16T + 4(l>>4) + r (r < 4) of point l & 15 -- which is both the B operand of the
@@ -366,8 +366,7 @@ static int mfma_min_chunks() {
 
 template <int DH>
 bool mfma_ok(const AttnApplyArgs& a, bool bwd) {
-  static const bool valu = std::getenv("GNOT_APPLY_VALU") != nullptr;
-  return !valu && a.nchunks >= mfma_min_chunks() && a.nsrc >= 1 && a.nsrc <= 8 && (a.ldq & 3) == 0 &&
+  return a.nchunks >= mfma_min_chunks() && a.nsrc >= 1 && a.nsrc <= 8 && (a.ldq & 3) == 0 &&
          (!bwd || ((a.lddq & 3) == 0 && (a.lddu & 3) == 0)) && apply_lds_bytes<DH>(a.nsrc, a.H, bwd) <= kApplyLdsMax;
 }
 
@@ -426,8 +425,7 @@ hipError_t launch_kv(const AttnKVBwdArgs* a, const AttnKVBwdArgs* jobs_dev, int 
 // hipErrorNotSupported when the head width / LDS size has no MFMA variant
 hipError_t launch_attn_kv_bwd_mfma(const AttnKVBwdArgs* a, const AttnKVBwdArgs* jobs_dev, int njobs, int maxchunks,
                                    int H, int dh, hipStream_t s) {
-  static const bool valu = std::getenv("GNOT_APPLY_VALU") != nullptr;
-  if (valu || (a && ((a->ldkv & 3) || (a->lddkv & 3)))) return hipErrorNotSupported;
+  if (a && ((a->ldkv & 3) || (a->lddkv & 3))) return hipErrorNotSupported;
   if ((a ? a->nchunks : maxchunks * njobs) < mfma_min_chunks()) return hipErrorNotSupported;
   switch (dh) {
     case 16: if (apply_lds_bytes<16>(1, H, true) <= kApplyLdsMax) return launch_kv<16>(a, jobs_dev, njobs, maxchunks, H, s); break;

@@ -112,7 +112,8 @@ chain_fwd_kernel(ChainArgs a) {
     for (int T = 0; T < OTL; ++T)
 #pragma unroll
       for (int r = 0; r < 4; ++r) y[T][r] *= s;
-    store_rows<OTL>(y, a.Y + e * a.y_chain_stride, a.ldy, p, valid, a.out_dim, lane);
+    if (a.Y != nullptr)   // null: MoE recompute (the saves only)
+      store_rows<OTL>(y, a.Y + e * a.y_chain_stride, a.ldy, p, valid, a.out_dim, lane);
   } else {
     store_rows<OTL>(y, a.Y + e * a.y_chain_stride, a.ldy, p, valid, a.out_dim, lane);
   }

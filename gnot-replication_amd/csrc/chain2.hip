@@ -22,51 +22,20 @@
 #include "gnot_kernels.h"
 #include "x6_core.h"
 
-#ifndef GNOT_C2_AHEAD_F
-#define GNOT_C2_AHEAD_F true
-#endif
-#ifndef GNOT_C2F_DMA_UNROLL
-#define GNOT_C2F_DMA_UNROLL 1
-#endif
-#ifndef GNOT_C2F_PAIR
-#define GNOT_C2F_PAIR 1        // forward pair mode (two output tiles per chunk): 0 never, 1 bf16 mode, 2 always
-#endif
-#ifndef GNOT_C2B_PRE
-#define GNOT_C2B_PRE 0
-#endif
-#ifndef GNOT_C2_AHEAD_B
-#define GNOT_C2_AHEAD_B true
-#endif
-// backward: weight chunks in flight ahead of the one being consumed (1 .. kC2Ring - 1), per arithmetic:
-// bf16x6 (NP = 3) and one-piece bf16 (NP = 1)
-#ifndef GNOT_C2B_LEAD_X6
-#define GNOT_C2B_LEAD_X6 1        // in-step (r03x): lead 1 232.2 ms, lead 2 235.0, lead 3 234.7 (concurrent weight gradients)
-#endif
-#ifndef GNOT_C2B_LEAD_B
-#define GNOT_C2B_LEAD_B 3
-#endif
-template <int NP>
-constexpr int c2b_lead() { return NP == 3 ? GNOT_C2B_LEAD_X6 : GNOT_C2B_LEAD_B; }
-#ifndef GNOT_C2B_PAIR
-#define GNOT_C2B_PAIR 1        // bf16-storage backward: two output tiles per weight chunk (one wait + barrier)
-#endif
-// output tiles per weight chunk of the backward (the bf16-storage chains' pair mode; the ring buffers
-// of the one-piece chains already hold two tiles, C2Lds::WB)
-template <int NP, bool B16>
-constexpr int c2b_ch() { return (B16 && NP == 1 && GNOT_C2B_PAIR) ? 2 : 1; }
-#ifndef GNOT_C2B_K
-#define GNOT_C2B_K 6           // bf16-storage backward: saved-row tile pairs requested this many pairs ahead (<= 6)
-#endif
-#ifndef GNOT_C2_B16_WPE
-#define GNOT_C2_B16_WPE 0      // bf16-storage chain kernels: waves per SIMD asked of the register allocator (0: none)
-#endif
-#if GNOT_C2_B16_WPE
-#define GNOT_C2_WPE(B16_) __attribute__((amdgpu_waves_per_eu((B16_) ? GNOT_C2_B16_WPE : 1)))
-#else
-#define GNOT_C2_WPE(B16_)
-#endif
-
 namespace gnot {
+
+// backward: weight chunks in flight ahead of the one being consumed (1 .. kC2Ring - 1), per arithmetic.
+// In-step (r03x): bf16x6 lead 1 / 2 / 3 = 232.2 / 235.0 / 234.7 ms per configs[2] step (the concurrent
+// weight gradients take the slack); the one-piece bf16 chains lead 3 (a tile's MFMA work is far shorter
+// than a chunk's L2 -> LDS latency)
+template <int NP>
+constexpr int c2b_lead() { return NP == 3 ? 1 : 3; }
+// output tiles per weight chunk of the backward: two in the bf16-storage chains (one counted wait and
+// barrier per pair; the ring buffers of the one-piece chains already hold two tiles, C2Lds::WB)
+template <int NP, bool B16>
+constexpr int c2b_ch() { return (B16 && NP == 1) ? 2 : 1; }
+// bf16-storage backward: saved-row tile pairs requested this many pairs ahead (r03r: 6 vs 1 neutral)
+constexpr int kC2bPairsAhead = 6;
 
 
 // LDS of one workgroup (u32x4 units): two weight-chunk buffers, two 1 KiB bias buffers (layer parity,
@@ -74,7 +43,7 @@ namespace gnot {
 // forward pair mode: two output tiles per weight chunk, one barrier per pair.  Measured (`r02bf`):
 // bf16 mode chain forward 348 -> 388 TFLOP/s; bf16x6 unchanged (202), so only the one-piece mode
 template <int NP>
-constexpr bool c2f_pair() { return GNOT_C2F_PAIR == 2 || (GNOT_C2F_PAIR == 1 && NP == 1); }
+constexpr bool c2f_pair() { return NP == 1; }
 
 template <int D, int NP>
 struct C2Lds {
@@ -83,11 +52,94 @@ struct C2Lds {
   static constexpr int kBias = kC2Ring * WB;            // offset of the bias buffers
   static constexpr int kHs = kBias + 2 * 64;            // offset of the saved-row slots
   // saved-row slots per wave: 4 (bf16x6), 8 at one piece (the bf16-storage backward keeps up to
-  // GNOT_C2B_K + 1 tile pairs in flight; a power of two dividing the 8 pairs of a layer)
+  // kC2bPairsAhead + 1 tile pairs in flight; a power of two dividing the 8 pairs of a layer)
   static constexpr int kSlots = NP == 1 ? 8 : 4;
   static constexpr int kBytes = (kHs + kC2Waves * kSlots * 64) * 16;
 };
 
+
+// ------------------------------------------------------------------------------ expert grid and combine
+// Workgroup -> (128-point block, expert).  Workgroups are dealt round-robin over the 8 XCDs (w and w + 8
+// share one, MI355X_MICROARCH.md "Workgroup dispatch"), so the E experts of a block are given ids
+// w = 8 (E (b / 8) + e) + b % 8: they run at the same time on CUs of ONE XCD, read the block's input rows
+// (forward: the MoE input; backward: dquery, the scores) once from HBM into that XCD's L2, and the fused
+// combine below reads their stage rows while they are fresh.  Speed only: nothing depends on placement.
+// The walk form (one workgroup per block, all experts) and single chains keep blockIdx.x.
+GNOT_DEV void c2_grid_pos(int E, bool grouped, int& blk, int& e) {
+  if (!grouped) {
+    blk = (int)blockIdx.x;
+    e = 0;
+    return;
+  }
+  const int w = (int)blockIdx.x, s = w >> 3;
+  e = s % E;
+  blk = (s / E) * 8 + (w & 7);
+}
+// grid of the expert grid: ceil(blocks / 8) * 8 * E workgroups (the ids past the last block exit at once)
+inline unsigned c2_grid_size(int nblocks, int E, bool grouped) {
+  return grouped ? (unsigned)((nblocks + 7) / 8 * 8) * (unsigned)E : (unsigned)nblocks;
+}
+
+// OT point-form tiles of this lane's row (rows of 256 fp32, voff = row-in-block * 1 KiB + 16 B * g) stored
+// write-through (sc1: the bytes reach the device-coherent level, so another XCD's sc1 loads see them)
+template <int OT>
+GNOT_DEV void store_rows_sc1(const float (&v)[OT][4], rsrc_t r, int voff) {
+#pragma unroll
+  for (int T = 0; T < OT; ++T)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, make_float4(v[T][0], v[T][1], v[T][2], v[T][3])),
+                                           r, voff + 64 * T, 0, kCpolSc1);
+}
+
+// The fused soft-MoE combine (model.py:128-131 / 134-137): called by every workgroup of the expert grid
+// after its write-through stage stores.  Hand-off (MI355X_MICROARCH.md, "Valid forms", first table row):
+// every wave waits for its own stores (vmcnt(0)), a barrier, then ONE lane adds to the block's counter
+// (agent scope) for the whole workgroup; the workgroup whose add returns E - 1 is the last, resets the
+// counter for the next launch and, after a barrier, sums the block's E stage rows with sc1 loads, in
+// expert order, onto `base` (or 0): bitwise the separate combine pass it replaces.  One workgroup per CU
+// (the chain kernels' LDS), as that hand-off form requires.
+GNOT_DEV void moe_combine_last(const float* stage, long stage_stride, int E, const float* base, float* out,
+                               int* counters, int blk, long row0, int nrows) {
+  __shared__ int last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int old = __hip_atomic_fetch_add(counters + blk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == E - 1;
+    if (old == E - 1) __hip_atomic_store(counters + blk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!last) return;
+  // 128 rows x 64 float4: thread t owns column group t & 63 of rows (t >> 6) + 8 k, two rows per round
+  // with every expert's loads in flight (rows past the block's nrows read 0, their stores are dropped)
+  const unsigned bytes = (unsigned)nrows * 1024u;
+  const long fo = row0 * 256;
+  const rsrc_t ro = make_rsrc(out + fo, bytes);
+  const rsrc_t rb = make_rsrc(base ? base + fo : out + fo, base ? bytes : 0u);
+  const int t = threadIdx.x, c16 = (t & 63) * 16, r0 = t >> 6;
+  for (int k = 0; k < 16; k += 2) {
+    const int vo0 = (r0 + 8 * k) * 1024 + c16, vo1 = vo0 + 8 * 1024;
+    float4 acc0 = base ? buf_load_f32x4(rb, vo0, 0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 acc1 = base ? buf_load_f32x4(rb, vo1, 0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int e0 = 0; e0 < E; e0 += 8) {
+      float4 s0[8], s1[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (e0 + j < E) {
+          const rsrc_t rs = make_rsrc(stage + (e0 + j) * stage_stride + fo, bytes);
+          s0[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo0, 0, kCpolSc1));
+          s1[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo1, 0, kCpolSc1));
+        }
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (e0 + j < E) {
+          acc0.x += s0[j].x; acc0.y += s0[j].y; acc0.z += s0[j].z; acc0.w += s0[j].w;
+          acc1.x += s1[j].x; acc1.y += s1[j].y; acc1.z += s1[j].z; acc1.w += s1[j].w;
+        }
+    }
+    buf_store_f32x4(acc0, ro, vo0);
+    buf_store_f32x4(acc1, ro, vo1);
+  }
+}
 
 // ------------------------------------------------------------------------------------------ forward
 // One forward layer: OT output tiles h = W a + b of the split input `in`; saves h (SAVE) and returns
@@ -168,7 +220,7 @@ GNOT_DEV void c2f_layer(C2Pipe& pp, const u32x4* W, const u32x4 (&in)[KBI][NP], 
       if (o > 0) {
         const f32x4 pv = prev;
         auto ep = [&](int r) { epi_part(o - 1, pv, r); };
-        acc = c2_tile_epi<KBI, NP, GNOT_C2_AHEAD_F>(cb, in, __builtin_bit_cast(f32x4, bb), pp.lane, ep, issue);
+        acc = c2_tile_epi<KBI, NP, true>(cb, in, __builtin_bit_cast(f32x4, bb), pp.lane, ep, issue);
       } else {
         issue();
         acc = c2_tile<KBI, false, NP>(cb, in, __builtin_bit_cast(f32x4, bb), pp.lane);
@@ -179,7 +231,7 @@ GNOT_DEV void c2f_layer(C2Pipe& pp, const u32x4* W, const u32x4 (&in)[KBI][NP], 
       const u32x4 bb = bias[4 * (o + 1) + g];
       const f32x4 pv = prev;
       auto ep = [&](int r) { epi_part(o, pv, r); };
-      prev = c2_tile_epi<KBI, NP, GNOT_C2_AHEAD_F>(cb + TU, in, __builtin_bit_cast(f32x4, bb), pp.lane, ep);
+      prev = c2_tile_epi<KBI, NP, true>(cb + TU, in, __builtin_bit_cast(f32x4, bb), pp.lane, ep);
     }
   }
   epi(OT - 1, prev);
@@ -194,11 +246,7 @@ GNOT_DEV void c2f_layer(C2Pipe& pp, const u32x4* W, const u32x4 (&in)[KBI][NP], 
     ++pp.cnt;
     auto issue = [&]() __attribute__((always_inline)) {
       if (o + 1 < OT) {
-#if GNOT_C2F_DMA_UNROLL
         dma_image_n<TU, kC2Waves>(nb, W + (size_t)(o + 1) * TU, pp.wave, pp.lane);
-#else
-        dma_image(nb, W + (size_t)(o + 1) * TU, TU, kC2Waves, pp.wave, pp.lane);
-#endif
       } else if (nextW) {
         // the next layer's bias first: the next layer's first wait only counts ops after its weights
         if (pp.wave == 0)
@@ -212,7 +260,7 @@ GNOT_DEV void c2f_layer(C2Pipe& pp, const u32x4* W, const u32x4 (&in)[KBI][NP], 
     if (o > 0) {
       const f32x4 pv = prev;
       auto ep = [&](int r) { epi_part(o - 1, pv, r); };
-      acc = c2_tile_epi<KBI, NP, GNOT_C2_AHEAD_F>(cb, in, __builtin_bit_cast(f32x4, bb), pp.lane, ep, issue);
+      acc = c2_tile_epi<KBI, NP, true>(cb, in, __builtin_bit_cast(f32x4, bb), pp.lane, ep, issue);
     } else {
       issue();
       acc = c2_tile<KBI, false, NP>(cb, in, __builtin_bit_cast(f32x4, bb), pp.lane);
@@ -230,18 +278,21 @@ GNOT_DEV void c2f_layer(C2Pipe& pp, const u32x4* W, const u32x4 (&in)[KBI][NP], 
 // B16 (bf16 mode, ChainArgs::b16s): bf16 pair-interleaved saves, plus each Linear's RNE bf16 input (the
 // split the MFMAs consume, stored as it is made) for the weight gradients
 template <int D, int KT0, int OTL, bool SAVE, int NP, bool WALK, bool B16 = false>
-__global__ void __launch_bounds__(64 * kC2Waves) GNOT_C2_WPE(B16) chain2_fwd_kernel(ChainArgs a) {
+__global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) {
   constexpr int DT = D / 16, KB = DT / 2, KB0 = (KT0 + 1) / 2;
   using LD = C2Lds<D, NP>;
   extern __shared__ __attribute__((aligned(16))) u32x4 c2lds[];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4;
-  const long p = ((long)blockIdx.x * kC2Waves + wave) * 16 + (lane & 15);
+  int blk, eg;
+  c2_grid_pos(a.nchains, !WALK && a.nchains > 1, blk, eg);
+  if ((long)blk * kC2Waves * 16 >= a.P) return;       // past the last block (whole workgroup, before any barrier)
+  const long p = ((long)blk * kC2Waves + wave) * 16 + (lane & 15);
   const bool valid = p < a.P;
   const int nl = a.nlin;
   // Every buffer resource of a layer starts at this workgroup's first row (64-bit base in SGPRs), so the
   // 32-bit offsets only span the workgroup's 128 rows: no bound on the point count of a launch.  Rows
   // past P read 0 / are dropped by the resource's bound (the workgroup's rows that exist).
-  const long row0 = (long)blockIdx.x * kC2Waves * 16;
+  const long row0 = (long)blk * kC2Waves * 16;
   const int nrows = (int)min((long)kC2Waves * 16, (long)a.P - row0);
   const unsigned lay_bytes = (unsigned)nrows * (unsigned)(D * 4);   // this workgroup's rows of a [P, D] layer
   // byte offset of this lane's row within the workgroup's rows
@@ -292,7 +343,7 @@ __global__ void __launch_bounds__(64 * kC2Waves) GNOT_C2_WPE(B16) chain2_fwd_ker
     int pend0 = 0;
     if constexpr (B16) {
       // the shared MoE input (Linear 0's operand): chain 0 only
-      if (WALK ? e == 0 : blockIdx.y == 0) {
+      if (e == 0) {
         if constexpr (KB0 == KB) pend0 = store_in(a.save + nl * a.save_layer_stride, b0, KB0);
       }
     }
@@ -375,13 +426,21 @@ __global__ void __launch_bounds__(64 * kC2Waves) GNOT_C2_WPE(B16) chain2_fwd_ker
 #pragma unroll
       for (int r = 0; r < 4; ++r) y[T][r] *= s;
   }
-  store_rows<OTL>(y, a.Y + e * a.y_chain_stride, a.ldy, p, valid, a.out_dim, lane);
+  if constexpr (OTL == 16) {
+    if (a.combine != nullptr) {               // fused combine: write-through stage rows (D = 256)
+      store_rows_sc1<OTL>(y, make_rsrc(a.Y + e * a.y_chain_stride + row0 * D, lay_bytes), voff);
+      return;
+    }
+  }
+  if (a.Y != nullptr) store_rows<OTL>(y, a.Y + e * a.y_chain_stride, a.ldy, p, valid, a.out_dim, lane);
   }
   };
   if constexpr (WALK) {
     for (int e = 0; e < a.nchains; ++e) expert(e);
   } else {
-    expert((int)blockIdx.y);
+    expert(eg);
+    if (a.combine != nullptr)
+      moe_combine_last(a.Y, a.y_chain_stride, a.nchains, a.base, a.combine, a.counters, blk, row0, nrows);
   }
 }
 
@@ -401,12 +460,12 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP],
                         float (&nx)[16][4]) {
   constexpr int DT = 16, TU = c2_tile_u4(KBI, NP), LEAD = c2b_lead<NP>(), CH = c2b_ch<NP, B16>(), NC = DT / CH;
   static_assert(LEAD >= 1 && LEAD < kC2Ring, "weight ring too small");
-  static_assert(CH == 1 || (B16 && GNOT_C2B_K >= LEAD), "pair mode: a pair's saved rows must be requested no later "
-                                                         "than the chunk whose wait retires them");
+  static_assert(CH == 1 || (B16 && kC2bPairsAhead >= LEAD), "pair mode: a pair's saved rows must be requested no "
+                                                             "later than the chunk whose wait retires them");
   constexpr int SL = C2Lds<256, NP>::kSlots;
   // B16: pairs requested PK pairs ahead (pair m of a layer in slot m % SL; the next layer's pairs
   // continue the numbering, SL divides the 8 pairs of a layer); fp32 saves: tiles two ahead
-  constexpr int PK = B16 ? GNOT_C2B_K : 1;
+  constexpr int PK = B16 ? kC2bPairsAhead : 1;
   static_assert(!B16 || (PK >= 1 && PK + 2 <= SL), "slot ring too small for the prefetch distance");
   u32x4* slots = pp.lds + C2Lds<256, NP>::kHs + pp.wave * SL * 64;
   const int g = pp.lane >> 4;
@@ -493,12 +552,10 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP],
       read_h(o - 1);
       const f32x4 pv = prev;
       auto ep = [&](int r) { epi_part(o - 1, pv, r); };
-#if GNOT_C2B_PRE
-      acc = c2_tile_epi<KBI, NP, GNOT_C2_AHEAD_B>(cb, in, f32x4{0.f, 0.f, 0.f, 0.f}, pp.lane, ep, issue);
-#else
+      // the DMA issue first, then the tile (issuing it after k-block 0's fragment reads, as the forward
+      // does, measured 155.0 -> 152.3 TFLOP/s here, r02ax)
       issue();
-      acc = c2_tile_epi<KBI, NP, GNOT_C2_AHEAD_B>(cb, in, f32x4{0.f, 0.f, 0.f, 0.f}, pp.lane, ep);
-#endif
+      acc = c2_tile_epi<KBI, NP, true>(cb, in, f32x4{0.f, 0.f, 0.f, 0.f}, pp.lane, ep);
     } else {
       issue();
       acc = c2_tile<KBI, false, NP>(cb, in, f32x4{0.f, 0.f, 0.f, 0.f}, pp.lane);
@@ -517,16 +574,19 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP],
 // in place (expert e > 0 reads back the partial this lane stored for e-1), no stage, no combine pass.
 // B16 (bf16 mode, ChainArgs::b16s): saves and dz as bf16 pair-interleaved rows
 template <int D, int KT0, int OTL, int NP, bool WALK, bool B16 = false>
-__global__ void __launch_bounds__(64 * kC2Waves) GNOT_C2_WPE(B16) chain2_bwd_kernel(ChainArgs a) {
+__global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) {
   constexpr int DT = D / 16, KB = DT / 2, KBL = (OTL + 1) / 2;
   using LD = C2Lds<D, NP>;
   extern __shared__ __attribute__((aligned(16))) u32x4 c2lds[];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4;
-  const long p = ((long)blockIdx.x * kC2Waves + wave) * 16 + (lane & 15);
+  int blk, eg;
+  c2_grid_pos(a.nchains, !WALK && a.nchains > 1, blk, eg);
+  if ((long)blk * kC2Waves * 16 >= a.P) return;       // past the last block (whole workgroup, before any barrier)
+  const long p = ((long)blk * kC2Waves + wave) * 16 + (lane & 15);
   const bool valid = p < a.P;
   const int nl = a.nlin;
   // buffer resources start at this workgroup's first row (chain2_fwd_kernel): 32-bit offsets span 128 rows
-  const long row0 = (long)blockIdx.x * kC2Waves * 16;
+  const long row0 = (long)blk * kC2Waves * 16;
   const int nrows = (int)min((long)kC2Waves * 16, (long)a.P - row0);
   const unsigned lay_bytes = (unsigned)nrows * (unsigned)(D * 4);
   const int voff = (int)(((unsigned)wave * 16u + (unsigned)(lane & 15)) * (unsigned)(D * 4) + 16u * (unsigned)g);
@@ -549,15 +609,15 @@ __global__ void __launch_bounds__(64 * kC2Waves) GNOT_C2_WPE(B16) chain2_bwd_ker
   auto rh = [&](int l) { return make_rsrc(save + l * a.save_layer_stride + rbase, lb); };   // h_l
   auto rz = [&](int l) { return make_rsrc(dz + l * a.dz_layer_stride + rbase, lb); };      // dz_l
   // prologue DMA: the last Linear's first c2b_lead<NP>() weight chunks (ring buffers 0 ..) and the first
-  // two h_{nl-2} tiles (B16: pairs 0 .. GNOT_C2B_K - 1)
+  // two h_{nl-2} tiles (B16: pairs 0 .. kC2bPairsAhead - 1)
   // (h first: a chunk's counted wait retires only the ops older than its DMA)
   {
     u32x4* slots = c2lds + LD::kHs + wave * LD::kSlots * 64;
     const rsrc_t r = rh(nl - 2);
     if constexpr (B16) {
 #pragma unroll
-      for (int m = 0; m < GNOT_C2B_K; ++m) dma16(r, slots + m * 64, rowb + 16 * g, 64 * m);
-      pp.issued += GNOT_C2B_K;
+      for (int m = 0; m < kC2bPairsAhead; ++m) dma16(r, slots + m * 64, rowb + 16 * g, 64 * m);
+      pp.issued += kC2bPairsAhead;
     } else {
       dma16(r, slots, voff, 0);
       dma16(r, slots + 64, voff, 64);
@@ -668,6 +728,8 @@ __global__ void __launch_bounds__(64 * kC2Waves) GNOT_C2_WPE(B16) chain2_bwd_ker
           for (int r = 0; r < 4; ++r) dx[T][r] += part[T][r];
       }
       store_rows<KT0>(dx, a.dX, a.lddx, p, valid, a.in_dim, lane);
+    } else if (KT0 == 16 && a.combine != nullptr) {   // fused combine: write-through stage rows (D = 256)
+      store_rows_sc1<KT0>(dx, make_rsrc(a.dX + e * a.dx_chain_stride + row0 * D, lay_bytes), voff);
     } else {
       store_rows<KT0>(dx, a.dX + e * a.dx_chain_stride, a.lddx, p, valid, a.in_dim, lane);
     }
@@ -676,14 +738,20 @@ __global__ void __launch_bounds__(64 * kC2Waves) GNOT_C2_WPE(B16) chain2_bwd_ker
   if constexpr (WALK) {
     for (int e = 0; e < a.nchains; ++e) expert(e);
   } else {
-    expert((int)blockIdx.y);
+    expert(eg);
+    if (a.combine != nullptr)
+      moe_combine_last(a.dX, a.dx_chain_stride, a.nchains, nullptr, a.combine, a.counters, blk, row0, nrows);
   }
 }
 
 template <int D, int NP>
 static hipError_t launch_chain2_d(const ChainArgs& a, bool bwd, hipStream_t s) {
   constexpr int DT = D / 16;
-  const dim3 grid((a.P + 16 * kC2Waves - 1) / (16 * kC2Waves), a.walk ? 1 : a.nchains), block(64 * kC2Waves);
+  const int nblocks = (a.P + 16 * kC2Waves - 1) / (16 * kC2Waves);
+  const dim3 grid(c2_grid_size(nblocks, a.nchains, !a.walk && a.nchains > 1)), block(64 * kC2Waves);
+  if (a.combine != nullptr && (a.walk || a.mode != CH_MOE || a.KT0 != DT || a.OTL != DT || !a.counters ||
+                               (bwd ? (!a.dX || a.lddx != D || a.dx_chain_stride % 4) : (!a.Y || a.ldy != D || a.y_chain_stride % 4))))
+    return hipErrorInvalidValue;
   const size_t lds = C2Lds<D, NP>::kBytes;
 #define GNOT_C2_ATTR(K)                                                                                  \
   do {                                                                                                   \

@@ -193,10 +193,7 @@ struct gnot_plan {
   int np = 3;
   // bf16 mode stores the soft-MoE chains' saves and dZ as bf16 (ChainArgs::b16s): one [P, 256] bf16 layer
   // is P * D / 2 four-byte units, a chain's 2 * NL save slots take what NL fp32 layers did
-  bool b16s() const {
-    static const bool off = std::getenv("GNOT_NO_B16S") != nullptr;   // A/B: bf16 mode with fp32 storage
-    return np == 1 && D == 256 && !off;
-  }
+  bool b16s() const { return np == 1 && D == 256; }
   std::string msave(int l, bool m1) const {
     return moe_recompute ? std::string("mrsave") : "b" + std::to_string(l) + (m1 ? ".m1save" : ".m2save");
   }
@@ -539,9 +536,7 @@ static void plan_images(gnot_plan* p) {
 
 // ====================================================================== point-reduction GEMM groups
 static void finish_group(gnot_plan* p, WgradGroup& G) {
-  // env GNOT_WGRAD_FP32: weight gradients on the fp32 MFMA kernel (diagnostics)
-  static const bool fp32_only = std::getenv("GNOT_WGRAD_FP32") != nullptr;
-  G.x6 = !fp32_only;
+  G.x6 = true;
   for (const auto& J : G.jobs)
     if (J.w != nullptr || J.state_dh > 0 || J.diag_only) G.x6 = false;
   // the x6 kernel holds ~240 registers per lane: one workgroup per CU leaves the other half of
@@ -550,9 +545,8 @@ static void finish_group(gnot_plan* p, WgradGroup& G) {
   // d = 256: every job's whole 256 x 256 gradient in one workgroup (8 waves, 96 KiB LDS: one per CU).
   // The split-K target is fixed (r02bh: 192-512 all within noise), so the split counts the parity
   // tests exercise are the ones every run uses
-  static const bool no_wide = std::getenv("GNOT_NO_WIDE") != nullptr;
   constexpr long wide_wgs = 256;
-  G.wide = G.x6 && !no_wide && p->D == 256 && !G.jobs.empty();
+  G.wide = G.x6 && p->D == 256 && !G.jobs.empty();
   for (const auto& J : G.jobs)
     if (J.out > 256 || J.in > 256) G.wide = false;
   if (G.b16) G.wide = true;          // the bf16-storage kernel has the wide kernel's geometry
@@ -594,14 +588,13 @@ static void finish_group(gnot_plan* p, WgradGroup& G) {
 
 // attention-state group (state.hip): one job per sample, ceil(P / kStatePts) partial states each
 static void finish_state_group(gnot_plan* p, WgradGroup& G) {
-  static const int env_pts = std::getenv("GNOT_STATE_PTS") ? std::atoi(std::getenv("GNOT_STATE_PTS")) : 0;
   if (!G.jobs.empty()) {
     const int d = G.jobs[0].out;
     const int dh = G.jobs[0].state_dh;
     long total = 0;
     for (const auto& J : G.jobs) total += J.P;
     G.state_mfma = state_mfma_ok(d, dh) && total >= state_mfma_min_points();
-    G.state_pts = env_pts > 0 ? (G.state_mfma ? env_pts : std::min(env_pts, 8192 / d)) : state_pts(G.state_mfma, d);
+    G.state_pts = state_pts(G.state_mfma, d);
     G.state_nw = 0;
     for (const auto& J : G.jobs)
       if (J.w != nullptr) G.state_nw = d / J.state_dh;
@@ -1131,6 +1124,8 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
   }
   p->moe_walk = p->D == 256 && p->L > 0 && chain2_walk_choice(P, E);
   if (!p->moe_walk) C.add("stage", E * P * D, D);
+  if (p->D == 256 && p->L > 0 && !p->moe_walk)        // fused-combine completion counters, one per 128 points
+    C.add("moe_cnt", (P + 127) / 128, 0);
   if (tr && p->moe_recompute && p->L > 0) C.add("mrsave", E * NL * P * D, D);
   if (p->sharded) {                          // scramble exchange scratch: head-major rows / packed peers
     C.add("xa", P * D, D);
@@ -1380,16 +1375,14 @@ extern "C" int gnot_plan_bind_workspace_async(gnot_plan* p, void* workspace, siz
     GNOT_CK(hipEventRecord(p->stage_ev[k], s));
     p->stage_used[k] = true;
   }
+  // the fused soft-MoE combine's completion counters start at zero (each launch leaves them at zero)
+  if (p->bufs.count("moe_cnt"))
+    GNOT_CK(hipMemsetAsync(p->P_("moe_cnt"), 0, ((p->P + 127) / 128) * sizeof(int), static_cast<hipStream_t>(stream)));
   if (!p->side2) GNOT_CK(hipStreamCreateWithFlags(&p->side2, hipStreamNonBlocking));
   if (!p->side) {
     // same priority as the caller's stream: measured on MI355X, a low- (or high-) priority side
-    // stream serialises against the main one and the step takes ~1.9x longer (GNOT_SIDE_PRIO)
-    int least = 0, greatest = 0;
-    GNOT_CK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    const char* env = std::getenv("GNOT_SIDE_PRIO");
-    const int prio = env ? std::atoi(env) : 0;
-    if (std::getenv("GNOT_DEBUG_PRIO")) std::fprintf(stderr, "[gnot] stream priority range least=%d greatest=%d, side=%d\n", least, greatest, prio);
-    GNOT_CK(hipStreamCreateWithPriority(&p->side, hipStreamNonBlocking, prio));
+    // stream serialises against the main one and the step takes ~1.9x longer (round 1)
+    GNOT_CK(hipStreamCreateWithPriority(&p->side, hipStreamNonBlocking, 0));
   }
   while (p->evs.size() < 256) {
     hipEvent_t e;
@@ -1692,8 +1685,10 @@ int attn_backward(Ctx& c, int l, bool cross) {
 
 }  // namespace
 
-// the soft-MoE experts of one call: walk form (d = 256, chain2.hip) or the expert grid + moe_combine
+// the soft-MoE experts of one call: walk form (d = 256, chain2.hip) or the expert grid, whose last
+// workgroup per 128-point block sums the experts (the fused combine, d = 256) -- moe_combine at d < 256
 static bool moe_walk(gnot_plan* p) { return p->moe_walk; }
+static bool moe_fused(gnot_plan* p) { return p->D == 256 && !p->moe_walk; }
 // save (and dZ) layout of a soft-MoE chain call: fp32 [NL][P][D] per expert, or in bf16 mode 2 NL bf16
 // layers per expert (ChainArgs::b16s)
 static void moe_save_strides(gnot_plan* p, ChainArgs& a) {
@@ -1716,12 +1711,13 @@ static int moe_forward(Ctx& c, const ChainTable& T, const float* in, const float
     a.walk = 1; a.Y = qout; a.base = qin;
   } else {
     a.Y = p->P_("stage"); a.y_chain_stride = P * D;
+    if (moe_fused(p)) { a.base = qin; a.combine = qout; a.counters = reinterpret_cast<int*>(p->P_("moe_cnt")); }
   }
   {
     ProfScope ps(c, "moe_fwd", 2.0 * E * P * NL * (double)D * D);
     GNOT_CK(launch_chain_fwd(a, c.s));
   }
-  if (!walk) GNOT_CK(launch_moe_combine(qin, p->P_("stage"), P * D, E, qout, P * D, c.s));
+  if (!walk && !moe_fused(p)) GNOT_CK(launch_moe_combine(qin, p->P_("stage"), P * D, E, qout, P * D, c.s));
   return GNOT_OK;
 }
 
@@ -1737,8 +1733,7 @@ extern "C" int gnot_forward(gnot_plan* p, const float* x, const float* theta, co
   // the input-function branch (encoders, every block's K/V projections and states) depends only on
   // the input functions: it runs on side2 while the query branch (gating, x encoder) runs here.  The
   // query branch is issued first (graph replay dispatches in capture order).
-  static const bool no_fwd2 = std::getenv("GNOT_NO_SIDE2_FWD") != nullptr;
-  const bool br = p->I > 0 && !no_fwd2;
+  const bool br = p->I > 0;
   Ctx cf{p, br ? p->side2 : c.s};
   if (br) {
     hipEvent_t fork = next_event(p);
@@ -1878,9 +1873,9 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
         f.X = p->P_(s + (m1 ? "a" : "bb")); f.ldx = D; f.ldy = D;
         f.scores = p->P_("scores"); f.ldsc = (int)p->bufs["scores"].ld; f.mode = CH_MOE;
         f.save = mr; moe_save_strides(p, f);
-        // only the saves are needed: the walk form writes no output (Y = null), the expert grid its stage
+        // only the saves are needed: no output (Y = null), no combine
         f.walk = walk ? 1 : 0;
-        f.Y = walk ? nullptr : stage; f.y_chain_stride = P * D;
+        f.Y = nullptr; f.y_chain_stride = P * D;
         ProfScope ps(c, "moe_recompute", 2.0 * E * P * NL * (double)D * D);
         GNOT_CK(launch_chain_fwd(f, c.s));
       }
@@ -1889,25 +1884,23 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
       a.scores = p->P_("scores"); a.ldsc = (int)p->bufs["scores"].ld; a.dscore = p->P_("dscore");
       a.save = p->P_(p->msave(l, m1)); moe_save_strides(p, a);
       float* dsum = p->P_(p->dsum_buf(m1));
+      // d(MoE input) = sum_e W_e0^T dz_e0: summed in place by the walk form, by the expert grid's fused
+      // combine (d = 256), or by moe_combine over the stage
+      GNOT_RUN(guard_write(c, dsum));
       if (walk) {
-        // d(MoE input) = sum_e W_e0^T dz_e0 summed in place by the walk form (no stage, no combine)
-        GNOT_RUN(guard_write(c, dsum));
         a.walk = 1; a.dX = dsum; a.lddx = D; a.dx_chain_stride = 0;
       } else {
         a.dX = stage; a.lddx = D; a.dx_chain_stride = P * D;
+        if (moe_fused(p)) { a.combine = dsum; a.counters = reinterpret_cast<int*>(p->P_("moe_cnt")); }
       }
       GNOT_RUN(chain_bwd(a, m1 ? p->k_m1(l) : p->k_m2(l), P, m1 ? p->wg_m1[l] : p->wg_m2[l], "moe_bwd"));
-      if (!walk) {
-        GNOT_RUN(guard_write(c, dsum));
-        GNOT_CK(launch_moe_combine(nullptr, stage, P * D, E, dsum, P * D, c.s));
-      }
+      if (!walk && !moe_fused(p)) GNOT_CK(launch_moe_combine(nullptr, stage, P * D, E, dsum, P * D, c.s));
       // m2: self attention (model.py:133) ; m1: cross attention (model.py:127)
       GNOT_RUN(attn_backward(c, l, m1));
     }
   }
   // the input-function branch again runs on side2, concurrently with the query encoder and gating
-  static const bool no_bwd2 = std::getenv("GNOT_NO_SIDE2_BWD") != nullptr;
-  const bool br = p->I > 0 && !no_bwd2;
+  const bool br = p->I > 0;
   Ctx cf{p, br ? p->side2 : c.s};
   if (br) {
     hipEvent_t fork = next_event(p);

@@ -321,6 +321,9 @@ GNOT_DEV float u2f(unsigned x) { return __builtin_bit_cast(float, x); }
 // ---- buffer loads: base + bound in SGPRs (reads past `bytes` return 0), wave-uniform row offset in
 // an SGPR (soffset), only the lane's column offset in a VGPR
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
+// cache-policy operand of the buffer load / store builtins: sc1 (gfx950: write-through stores, L1-bypassing
+// loads -- the device-coherent form of an inter-workgroup hand-off, MI355X_MICROARCH.md)
+constexpr int kCpolSc1 = 16;
 // (base and bound are wave-uniform by construction; readfirstlane tells the compiler so, otherwise a
 // descriptor built from a value it cannot prove uniform is used inside a waterfall loop)
 GNOT_DEV rsrc_t make_rsrc(const void* p, unsigned bytes) {

@@ -94,7 +94,14 @@ struct ChainArgs {
   // dX = sum_e W_e0^T dz_e0 -- so no [P, E, d] stage and no combine pass (grid.y = 1).  Forward Y may
   // be null (MoE recompute: saves only).
   int walk = 0;
-  const float* base = nullptr;       // walk forward: the residual (query in); null = 0
+  const float* base = nullptr;       // forward: the residual (query in) of the walk form / the fused combine
+  // CH_MOE expert grid (walk = 0), d = 256: the fused soft-MoE combine.  The E workgroups of a 128-point
+  // block store their stage rows write-through and count their completions in counters[block]; the LAST
+  // one sums the block's E stage rows in expert order into `combine` (forward: base + sum_e s_e y_e,
+  // model.py:128-131; backward: d(MoE input) = sum_e dX_e) -- no separate combine pass.  counters: one
+  // int per 128-point block, zero between launches (each launch's last workgroups reset theirs)
+  float* combine = nullptr;
+  int* counters = nullptr;
   // CH_MOE, d = 256, np = 1 (bf16 mode): bf16 activation storage.  Saves and dZ are bf16 "pair-
   // interleaved" rows (gnot_common.h, 512 B per point; strides above then count 4-byte units, so a
   // [P, 256] bf16 layer is P * 128 of them).  Per chain, save slots 0 .. nlin-2 hold gelu'(h_l) of the
@@ -147,14 +154,11 @@ hipError_t launch_wgrad_b16(const WgradJob* jobs_dev, const int* wg_prefix_dev, 
 // Jobs are WgradJobs with state_dh > 0: A = dz/lddz, B = x/ldx, optional w/ldw, out = dW as
 // [H][dh*dh + dh], `splits` partials of state_pts(d) points each at slab + slab_off.
 // Two kernels: state_mfma (fp32 MFMA, rows straight from HBM, dh = 16/32/64 with H % 4 == 0;
-// env GNOT_STATE_VALU disables it) and the VALU state_partial (LDS-staged rows, any width).
-inline bool state_mfma_ok(int d, int dh) {
-  static const bool valu = std::getenv("GNOT_STATE_VALU") != nullptr;
-  return !valu && (dh == 16 || dh == 32 || dh == 64) && d % dh == 0 && (d / dh) % 4 == 0;
-}
+// below GNOT_STATE_MFMA_MIN points the VALU form) and the VALU state_partial (LDS-staged rows, any width).
+inline bool state_mfma_ok(int d, int dh) { return (dh == 16 || dh == 32 || dh == 64) && d % dh == 0 && (d / dh) % 4 == 0; }
 // points per partial-state workgroup: 256 on MFMA (4 waves per SIMD at 262k points, partials ~6 % of
 // the row bytes); VALU: the workgroup's A and B rows fill <= 32 KiB of LDS each (64 at d <= 128,
-// 8192 / d above; measured: 32 and 16 are slower at cfg2).  env GNOT_STATE_PTS overrides
+// 8192 / d above; measured: 32 and 16 are slower at cfg2)
 inline int state_pts(bool mfma, int d) { return mfma ? 256 : d <= 128 ? 64 : 8192 / d; }
 // MFMA only from this many points in the group (env GNOT_STATE_MFMA_MIN, read per plan): below it the
 // 256-point MFMA workgroups leave most CUs idle and the 64-point VALU kernel is faster (configs[1],

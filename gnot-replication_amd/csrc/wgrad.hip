@@ -389,15 +389,12 @@ GNOT_DEV void mfma_np(const u32x4 (&a)[NP], const u32x4 (&b)[NP], f32x16& c) {
   else c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[0]), __builtin_bit_cast(bf16x8, b[0]), c, 0, 0, 0);
 }
 
-// the wide kernel's row loads; GNOT_WGRAD_AUX: their cache-policy bits (0 default, 2 nt)
-#ifndef GNOT_WGRAD_AUX
-#define GNOT_WGRAD_AUX 0
-#endif
+// the wide kernel's row loads (default cache policy: nt measured within noise)
 GNOT_DEV float wrow_load(rsrc_t r, int voff, int soff) {
-  return u2f(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, GNOT_WGRAD_AUX));
+  return u2f(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
 }
 
-template <int V, int NP = 3>
+template <int NP = 3>
 __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __restrict__ jobs,
                                                               const int* __restrict__ prefix, int njobs,
                                                               float* __restrict__ slab) {
@@ -510,14 +507,11 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
     }
   };
 
-  // V & 1: the first half of the waves (w and w + 4 share a SIMD) runs at raised issue priority, so
-  //        after a barrier it gets through its MFMAs first and stages while its partner multiplies
-  // V & 2: two raw register sets (the rows of stage s+2 in flight for two stages)
-  // V & 4 (default): the staging of stage s+1 (GELU, split, LDS stores) and the row loads of stage s+2
-  //        are interleaved instruction by instruction with the MFMAs of stage s on the SAME wave, so
-  //        the VALU issues in the MFMA shadows instead of in a separate phase that both waves of a SIMD
-  //        reach together after every barrier (full 256 x 256 tiles; edge tiles take the plain loop)
-  if constexpr ((V & 4) != 0) {
+  // The staging of stage s+1 (GELU, split, LDS stores) and the row loads of stage s+2 are interleaved
+  // instruction by instruction with the MFMAs of stage s on the SAME wave, so the VALU issues in the MFMA
+  // shadows instead of in a separate phase that both waves of a SIMD reach together after every barrier
+  // (full 256 x 256 tiles; edge tiles take the plain double-buffered loop)
+  {
     if (pb >= pe) {
       // empty split: the partials below are zero
     } else {
@@ -616,47 +610,6 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
       }
       compute(buf);   // the last stage
     }
-  } else if constexpr ((V & 2) == 0) {
-    if ((V & 1) && wave < 4) __builtin_amdgcn_s_setprio(1);
-    Raw R;
-    if (pb < pe) {
-      load(R, pb);
-      stage(0, R);
-      if (pb + kWStage < pe) load(R, pb + kWStage);
-    }
-    __syncthreads();
-    int buf = 0;
-    for (long p0 = pb; p0 < pe; p0 += kWStage) {
-      compute(buf);
-      if (p0 + kWStage < pe) {
-        stage(buf ^ 1, R);
-        if (p0 + 2 * kWStage < pe) load(R, p0 + 2 * kWStage);
-      }
-      __syncthreads();
-      buf ^= 1;
-    }
-  } else {
-    if ((V & 1) && wave < 4) __builtin_amdgcn_s_setprio(1);
-    Raw R0, R1;
-    if (pb < pe) {
-      load(R0, pb);
-      if (pb + kWStage < pe) load(R1, pb + kWStage);
-      stage(0, R0);
-      if (pb + 2 * kWStage < pe) load(R0, pb + 2 * kWStage);
-    }
-    __syncthreads();
-    auto body = [&](long p0, int buf, Raw& Rn) {        // Rn: raw rows of stage p0 + kWStage
-      compute(buf);
-      if (p0 + kWStage < pe) {
-        stage(buf ^ 1, Rn);
-        if (p0 + 3 * kWStage < pe) load(Rn, p0 + 3 * kWStage);
-      }
-      __syncthreads();
-    };
-    for (long p0 = pb; p0 < pe; p0 += 2 * kWStage) {
-      body(p0, 0, R1);
-      if (p0 + kWStage < pe) body(p0 + kWStage, 1, R0);
-    }
   }
 
   // partials -> slab [split][128-tile][128 x (128 + 1)] (the pgemm_kernel layout)
@@ -677,7 +630,7 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
   if (J.db != nullptr) {
     // column sums of A: the two point halves of every feature through LDS, in a fixed order
     // (red overlays stage buffer 0, which other waves may still be reading in the last compute(): the
-    // V & 4 loop ends without a barrier)
+    // interleaved loop ends without a barrier)
     float* red = reinterpret_cast<float*>(wl);
     __syncthreads();
     red[hh * 256 + f] = dbacc;
@@ -896,23 +849,19 @@ hipError_t launch_wgrad(const WgradJob* jobs_dev, const int* wg_prefix_dev, int 
                         int np) {
   if (njobs <= 0) return hipSuccess;
   if (wide) {
-    // GNOT_X6W_VARIANT (diagnostics): 4 (default) staging interleaved with the MFMAs; 0 the plain double-buffered loop; 1 / 2 / 3 its priority-split / two-register-set
-    // forms (x6 only)
-    static const int var = std::getenv("GNOT_X6W_VARIANT") ? std::atoi(std::getenv("GNOT_X6W_VARIANT")) & 7 : 4;
-    const int v = np == 1 ? (var & 4) : var;
     const size_t lds = w_lds_bytes(np);
-#define GNOT_X6W(V_, NP_)                                                                                      \
-  if (v == V_ && np == NP_) {                                                                                  \
+#define GNOT_X6W(NP_)                                                                                          \
+  if (np == NP_) {                                                                                             \
     static bool attr = false;                                                                                  \
     if (!attr) {                                                                                               \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(pgemm_x6w_kernel<V_, NP_>),                      \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(pgemm_x6w_kernel<NP_>),                          \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                         \
       attr = true;                                                                                             \
     }                                                                                                          \
-    hipLaunchKernelGGL((pgemm_x6w_kernel<V_, NP_>), dim3(total_wgs), dim3(kWThreads), lds, s, jobs_dev,         \
+    hipLaunchKernelGGL((pgemm_x6w_kernel<NP_>), dim3(total_wgs), dim3(kWThreads), lds, s, jobs_dev,            \
                        wg_prefix_dev, njobs, slab);                                                            \
   }
-    GNOT_X6W(0, 3) GNOT_X6W(1, 3) GNOT_X6W(2, 3) GNOT_X6W(3, 3) GNOT_X6W(4, 3) GNOT_X6W(0, 1) GNOT_X6W(4, 1)
+    GNOT_X6W(3) GNOT_X6W(1)
 #undef GNOT_X6W
   } else if (x6)
     hipLaunchKernelGGL(pgemm_x6_kernel, dim3(total_wgs), dim3(256), 0, s, jobs_dev, wg_prefix_dev, njobs, slab);

@@ -140,16 +140,9 @@ struct C2Stream {
 // stores stay in flight across the barrier.
 template <int N>
 GNOT_DEV void c2_sync() {
-#ifdef GNOT_C2_SAFE
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#else
   asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
-#endif
 }
 GNOT_DEV void c2_sync_n(int n) {   // n is wave-uniform and small
-#ifdef GNOT_C2_SAFE
-  n = 0;
-#endif
   switch (n) {
     case 1: c2_sync<1>(); break;
     case 2: c2_sync<2>(); break;
