@@ -9,8 +9,9 @@ Default workload = BASELINE.json configs[2], the largest configuration that fits
 3-D mesh of 262,144 query points, GNOT with d=256, 8 experts, 8 heads, 4 blocks, 4-layer MLPs and one
 input function of 805 points, fp32 arithmetic (the reference computes in fp32; the MoE GEMMs run on
 bf16 MFMA with an exact three-piece split, fp32-level results).  A step = pack weights -> GNOT forward
-(gnot_amd, HIP) -> RelL2 loss (loss.py:14-23) -> backward to every parameter gradient -> (N>1: one
-RCCL all-reduce of the flat gradient buffer) -> AdamW step.
+(gnot_amd, HIP) -> RelL2 loss (loss.py:14-23) -> backward to every parameter gradient (N>1: summed
+over the ranks by RCCL group by group inside the backward, overlapped with it) -> AdamW step, captured
+in hipGraphs (RCCL kernels included).
 At N>1 ranks the default workload is configs[3], north_star's scaling target: ONE 1,048,576-point mesh
 point-sharded over the ranks (strong scaling: 1M / N points per GPU; every attention call all-reduces
 its states and runs the scramble all-to-all over RCCL).  --workload cfg3 at N>1
@@ -333,8 +334,10 @@ def main():
                                   "n_attn_hidden_dim", "n_mlp_num_layers", "n_mlp_hidden_dim",
                                   "n_input_hidden_dim", "n_expert", "n_head", "n_input_functions")]).to(device)
     shard = bool(w.get("shard") or w.get("shard_weak")) and (world > 1 or force_shard)
-    # the point-shard exchanges run inside the engine's launch sequence (RCCL through callbacks): eager
-    use_graph = not args.no_graph and not shard
+    # the point-shard exchanges run inside the engine's launch sequence (RCCL through callbacks on the
+    # engine's stream): RCCL kernels are graph-capturable, so the sharded step is captured too; the
+    # host-staged gloo rehearsal stays eager
+    use_graph = not args.no_graph and not (shard and backend != "nccl")
     from gnot_amd import train as gtrain
     # main.py:50-51 AdamW(lr=1e-3): one native update over the flat parameter arena (gnot_adamw_step),
     # or torch's fused multi-tensor AdamW (--torch-adamw; capturable keeps its step count on device)
@@ -371,13 +374,22 @@ def main():
         batches = [permuted_batch(D, k) for k in range(max(args.warmup, 2) + 3 + args.steps)]
         use_graph = False                         # every step binds a new geometry
     it = {"k": 0}
-    if shard:
+    comm = None
+    if world > 1 or shard:
         from gnot_amd import parallel as par
-        model.set_point_shard(par.PointShardComm(stage_via_host=backend != "nccl"))
+        comm = par.PointShardComm(stage_via_host=backend != "nccl")
+    if shard:
+        model.set_point_shard(comm)
+    if world > 1 and os.environ.get("GNOT_BENCH_FLAT_ALLREDUCE") != "1":
+        # the parameter gradients are summed over the ranks INSIDE the backward, one collective per weight-
+        # gradient group as soon as it is written (overlapped with the rest of the backward; SURVEY.md
+        # section 5); GNOT_BENCH_FLAT_ALLREDUCE=1: one all-reduce of the flat buffer after the backward
+        model.set_grad_allreduce(comm)
 
-    # one training step = [forward + RelL2 + backward] -> (N>1: ONE all-reduce (sum) of the flat
-    # gradient buffer) -> [AdamW].  With hipGraphs the two bracketed parts are captured once and
-    # replayed; the collective stays an eager RCCL call between them.
+    # one training step = [forward + RelL2 + backward (N>1: gradients summed over the ranks group by group
+    # inside it)] -> [AdamW].  With hipGraphs the two bracketed parts are captured once and replayed
+    # (RCCL kernels included); GNOT_BENCH_FLAT_ALLREDUCE=1 keeps one eager all-reduce of the flat gradient
+    # buffer between them instead.
     def fwd_bwd():
         nonlocal x, x_off, theta, fns, fn_offs, y
         if batches is not None:
@@ -403,7 +415,7 @@ def main():
             opt.launch(eng.grad_flat)
 
     def allreduce():
-        if world > 1:
+        if world > 1 and eng.grad_comm is None:
             dist.all_reduce(eng.grad_flat, op=dist.ReduceOp.SUM)
 
     def eager_step():
@@ -480,6 +492,8 @@ def main():
             "launches": M["klaunch"],
         }
 
+    M_graph = {"on": False}
+
     def measure():
         """warm-up, class profile, capture, K timed steps -> timing of the current precision"""
         # warm-up (also the capture warm-up: allocations, plan binding, optimizer state)
@@ -524,12 +538,18 @@ def main():
             eng.profile_enable(rkind)
             g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             print("[bench] capturing", file=sys.stderr, flush=True)
-            with torch.cuda.graph(g_fb):
-                fwd_bwd()
-            with torch.cuda.graph(g_opt, pool=g_fb.pool()):
-                opt_step()
-            torch.cuda.synchronize()
-            print("[bench] captured", file=sys.stderr, flush=True)
+            try:
+                with torch.cuda.graph(g_fb):
+                    fwd_bwd()
+                with torch.cuda.graph(g_opt, pool=g_fb.pool()):
+                    opt_step()
+                torch.cuda.synchronize()
+                captured = True
+            except Exception as ex:           # e.g. a collective the communicator cannot capture: stay eager
+                print(f"[bench] capture failed ({ex!r}); eager steps", file=sys.stderr, flush=True)
+                captured = False
+                torch.cuda.synchronize()
+            print("[bench] captured" if captured else "[bench] eager", file=sys.stderr, flush=True)
 
             def graph_step():
                 g_fb.replay()
@@ -537,7 +557,9 @@ def main():
                 if not args.torch_adamw:
                     opt.prepare()         # this step's AdamW hyper-parameters -> device (outside the graph)
                 g_opt.replay()
-            step = graph_step
+            if captured:
+                step = graph_step
+                M_graph["on"] = True
             for _ in range(2):
                 step()
             torch.cuda.synchronize()
@@ -590,7 +612,7 @@ def main():
                    "geometry": "new mesh order every step (--vary-geometry)" if batches is not None else "fixed",
                    "moe_recompute": recompute,
                    "parallelism": (f"point-shard{world}" if shard else f"sample-dp{world}") if (world > 1 or shard) else "single",
-                   "step": "pack+fwd+RelL2+bwd+AdamW (native loss, " + ("torch fused AdamW" if args.torch_adamw else "native flat AdamW") + ")" + (" (hipGraph replay)" if use_graph else " (eager)")},
+                   "step": "pack+fwd+RelL2+bwd+AdamW (native loss, " + ("torch fused AdamW" if args.torch_adamw else "native flat AdamW") + ")" + (" (hipGraph replay)" if M_graph["on"] else " (eager)")},
         "roofline": roofline(M0, args.dtype),
     }
     if (args.dtype == "fp32" and not args.fp32_only and world == 1 and m["n_attn_hidden_dim"] == 256

@@ -66,9 +66,9 @@ struct C2Lds {
 // combine below reads their stage rows while they are fresh.  Speed only: nothing depends on placement.
 // The walk form (one workgroup per block, all experts) and single chains keep blockIdx.x.
 GNOT_DEV void c2_grid_pos(int E, bool grouped, int& blk, int& e) {
-  if (!grouped) {
+  if (!grouped || gridDim.y > 1) {
     blk = (int)blockIdx.x;
-    e = 0;
+    e = (int)blockIdx.y;
     return;
   }
   const int w = (int)blockIdx.x, s = w >> 3;
@@ -109,35 +109,45 @@ GNOT_DEV void moe_combine_last(const float* stage, long stage_stride, int E, con
   }
   __syncthreads();
   if (!last) return;
-  // 128 rows x 64 float4: thread t owns column group t & 63 of rows (t >> 6) + 8 k, two rows per round
-  // with every expert's loads in flight (rows past the block's nrows read 0, their stores are dropped)
+  // 128 rows x 64 float4: thread t owns column group t & 63 of rows (t >> 6) + 8 k, four rows per round
+  // with every expert's loads in flight (up to 36 16-byte loads per lane: the stage rows come from the
+  // memory side, so the latency, not the bytes, sets the time); rows past the block's nrows read 0,
+  // their stores are dropped
+  constexpr int R = 4;
   const unsigned bytes = (unsigned)nrows * 1024u;
   const long fo = row0 * 256;
   const rsrc_t ro = make_rsrc(out + fo, bytes);
   const rsrc_t rb = make_rsrc(base ? base + fo : out + fo, base ? bytes : 0u);
   const int t = threadIdx.x, c16 = (t & 63) * 16, r0 = t >> 6;
-  for (int k = 0; k < 16; k += 2) {
-    const int vo0 = (r0 + 8 * k) * 1024 + c16, vo1 = vo0 + 8 * 1024;
-    float4 acc0 = base ? buf_load_f32x4(rb, vo0, 0) : make_float4(0.f, 0.f, 0.f, 0.f);
-    float4 acc1 = base ? buf_load_f32x4(rb, vo1, 0) : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int k = 0; k < 16; k += R) {
+    int vo[R];
+    float4 acc[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      vo[i] = (r0 + 8 * (k + i)) * 1024 + c16;
+      acc[i] = base ? buf_load_f32x4(rb, vo[i], 0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     for (int e0 = 0; e0 < E; e0 += 8) {
-      float4 s0[8], s1[8];
+      float4 s[8][R];
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         if (e0 + j < E) {
           const rsrc_t rs = make_rsrc(stage + (e0 + j) * stage_stride + fo, bytes);
-          s0[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo0, 0, kCpolSc1));
-          s1[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo1, 0, kCpolSc1));
+#pragma unroll
+          for (int i = 0; i < R; ++i)
+            s[j][i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo[i], 0, kCpolSc1));
         }
 #pragma unroll
       for (int j = 0; j < 8; ++j)
         if (e0 + j < E) {
-          acc0.x += s0[j].x; acc0.y += s0[j].y; acc0.z += s0[j].z; acc0.w += s0[j].w;
-          acc1.x += s1[j].x; acc1.y += s1[j].y; acc1.z += s1[j].z; acc1.w += s1[j].w;
+#pragma unroll
+          for (int i = 0; i < R; ++i) {
+            acc[i].x += s[j][i].x; acc[i].y += s[j][i].y; acc[i].z += s[j][i].z; acc[i].w += s[j][i].w;
+          }
         }
     }
-    buf_store_f32x4(acc0, ro, vo0);
-    buf_store_f32x4(acc1, ro, vo1);
+#pragma unroll
+    for (int i = 0; i < R; ++i) buf_store_f32x4(acc[i], ro, vo[i]);
   }
 }
 
@@ -303,6 +313,9 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) 
   // float offset of the workgroup's first row in a layer (fp32: D floats per row; B16: 512 B = 128 floats)
   const long rbase = row0 * (B16 ? kB16Row / 4 : D);
   C2Pipe pp{c2lds, LD::WB, 0, wave, lane};
+#ifdef GNOT_EXP_PRIO
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);     // EXPERIMENT: static priority for the second half
+#endif
   constexpr int CH = c2f_pair<NP>() ? 2 : 1;         // output tiles per weight chunk
   // a layer's first wait: the saves the previous layer issued after its last weight DMA (its last
   // tile's stream + the final epilogue; pair mode: its last pair's two tiles + the final epilogue)
@@ -596,6 +609,9 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) 
   const long rbase = row0 * (B16 ? kB16Row / 4 : D);
   const int lvoff = B16 ? rowb : voff;               // what the layers address rows with
   C2Pipe pp{c2lds, LD::WB, 0, wave, lane};
+#ifdef GNOT_EXP_PRIO
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);     // EXPERIMENT: static priority for the second half
+#endif
   constexpr int e_begin = 0;
   auto expert = [&](int e) __attribute__((always_inline)) {
   const ChainLayer* L = a.layers + e * nl;
@@ -748,7 +764,10 @@ template <int D, int NP>
 static hipError_t launch_chain2_d(const ChainArgs& a, bool bwd, hipStream_t s) {
   constexpr int DT = D / 16;
   const int nblocks = (a.P + 16 * kC2Waves - 1) / (16 * kC2Waves);
-  const dim3 grid(c2_grid_size(nblocks, a.nchains, !a.walk && a.nchains > 1)), block(64 * kC2Waves);
+  static const bool nogroup = std::getenv("GNOT_C2_NOGROUP") != nullptr;   // TEMP A/B
+  const bool grouped = !a.walk && a.nchains > 1 && !nogroup;
+  const dim3 grid = grouped ? dim3(c2_grid_size(nblocks, a.nchains, true)) : dim3(nblocks, a.walk ? 1 : a.nchains);
+  const dim3 block(64 * kC2Waves);
   if (a.combine != nullptr && (a.walk || a.mode != CH_MOE || a.KT0 != DT || a.OTL != DT || !a.counters ||
                                (bwd ? (!a.dX || a.lddx != D || a.dx_chain_stride % 4) : (!a.Y || a.ldy != D || a.y_chain_stride % 4))))
     return hipErrorInvalidValue;

@@ -64,6 +64,7 @@ struct WgradGroup {
   bool x6 = false;                   // plain weight-gradient jobs: the bf16x6 MFMA kernel
   bool wide = false;                 // ... on the 256 x 256-tile kernel (d = 256: one workgroup per job split)
   bool b16 = false;                  // bf16-storage jobs (bf16 mode soft-MoE): pgemm_b16_kernel, wide geometry
+  std::vector<int> lins;             // weight-gradient groups: the canonical Linears whose (dW, db) they write
   int state_pts = 0, state_nw = 0;
   bool state_mfma = false;   // state groups: points per workgroup, per-point weights (0 or H)
   WgradJob* d_jobs = nullptr;        // device copies (workspace tables)
@@ -149,6 +150,9 @@ struct gnot_plan {
   // double-buffered and guarded by the event of its last side-stream reader
   hipStream_t side = nullptr;
   hipStream_t side2 = nullptr;          // input-function branch, concurrent with the query branch
+  // weight gradients on the caller's stream (no side-stream overlap): env GNOT_SERIAL_WGRAD, read when
+  // the plan is created (so a test can build both forms in one process)
+  bool serial_wgrad = false;
   std::vector<hipEvent_t> evs;
   size_t ev_next = 0;
   // pinned staging ring for the table uploads of gnot_plan_bind_workspace_async: slot k is rewritten
@@ -176,6 +180,11 @@ struct gnot_plan {
   // point sharding (gnot_plan_set_shard): sample b's points are split over `world` ranks
   int world = 1, rank = 0;
   gnot_comm comm{};
+  // gradient all-reduce overlapped with the backward (gnot_plan_set_grad_comm): each weight-gradient
+  // group's (dW, db) ranges are summed over the ranks on `comm_stream` as soon as the group is written
+  gnot_comm grad_comm{};
+  bool grad_comm_on = false;
+  hipStream_t comm_stream = nullptr;
   std::vector<long> nglob;                 // [B] global points per sample (sharded batches)
   bool sharded = false;                    // world > 1 for the current batch
   // MoE activation recompute (gnot_plan_set_moe_recompute): training keeps only each MoE call's
@@ -316,6 +325,7 @@ extern "C" int gnot_plan_create(const gnot_config* cfg, gnot_plan** out) {
   }
   p->W.assign(p->n_lin(), nullptr);
   p->b.assign(p->n_lin(), nullptr);
+  if (const char* sw = std::getenv("GNOT_SERIAL_WGRAD")) p->serial_wgrad = sw[0] == '1';
   *out = p;
   return GNOT_OK;
 }
@@ -332,6 +342,7 @@ extern "C" void gnot_plan_destroy(gnot_plan* plan) {
     if (plan->stage[k]) (void)hipHostFree(plan->stage[k]);
   }
   if (plan->side) (void)hipStreamDestroy(plan->side);
+  if (plan->comm_stream) (void)hipStreamDestroy(plan->comm_stream);
   if (plan->side2) (void)hipStreamDestroy(plan->side2);
   delete plan;
 }
@@ -663,6 +674,7 @@ static void build_groups(gnot_plan* p) {
     J.db = grads + p->grad_off[2 * li + 1];
     J.P = (int)rows;
     G.jobs.push_back(J);
+    G.lins.push_back(li);
   };
   // chain c of a group: Linear j reads dZ_j from dz[(c*NL + j)*rows*D] and its input from the
   // chain input (j = 0) or gelu(saved pre-activation j-1)
@@ -981,6 +993,14 @@ extern "C" int gnot_plan_set_shard(gnot_plan* p, int rank, int world, int B, con
   p->rank = rank;
   p->comm = *comm;
   p->nglob.assign(n_global, n_global + B);
+  return GNOT_OK;
+}
+
+extern "C" int gnot_plan_set_grad_comm(gnot_plan* p, const gnot_comm* comm) {
+  if (!p) return fail(GNOT_E_INVALID, "null plan");
+  if (comm && !comm->allreduce_sum) return fail(GNOT_E_INVALID, "gnot_comm.allreduce_sum is required");
+  p->grad_comm_on = comm != nullptr;
+  p->grad_comm = comm ? *comm : gnot_comm{};
   return GNOT_OK;
 }
 
@@ -1520,12 +1540,32 @@ int launch_group(gnot_plan* p, const WgradGroup& G, float* slab, hipStream_t s) 
   return GNOT_OK;
 }
 
+// the group's gradient ranges summed over the ranks (gnot_plan_set_grad_comm) on the comm stream, once
+// the event `done` (the group's kernels) has passed: consecutive canonical Linears are adjacent in the
+// arena ((dW, db) per Linear), so a group is a few contiguous ranges, one collective each
+int grad_allreduce(gnot_plan* p, const WgradGroup& G, hipEvent_t done) {
+  GNOT_CK(hipStreamWaitEvent(p->comm_stream, done, 0));
+  std::vector<int> ls(G.lins);
+  std::sort(ls.begin(), ls.end());
+  float* grads = p->P_("grads");
+  for (size_t k = 0; k < ls.size();) {
+    size_t m = k + 1;
+    while (m < ls.size() && ls[m] == ls[m - 1] + 1) ++m;
+    const long lo = p->grad_off[2 * ls[k]];
+    const long hi = p->grad_off[2 * ls[m - 1] + 1] + p->lin_o[ls[m - 1]];
+    if (p->grad_comm.allreduce_sum(p->grad_comm.user, grads + lo, hi - lo, p->comm_stream) != 0)
+      return fail(GNOT_E_HIP, "gnot_comm.allreduce_sum (gradients) failed");
+    k = m;
+  }
+  return GNOT_OK;
+}
+
 // weight gradients: forked onto the side stream (off the critical path); `reads` are the main-stream
 // buffers the group consumes, guarded until it finishes
 int run_wgrad_side(Ctx& c, const WgradGroup& G, std::initializer_list<const float*> reads) {
   if (G.jobs.empty()) return GNOT_OK;
   gnot_plan* p = c.p;
-  static const bool serial = std::getenv("GNOT_SERIAL_WGRAD") != nullptr;   // diagnostics: no overlap
+  const bool serial = p->serial_wgrad;
   // Only the caller's (capture-origin) stream forks to the side stream.  A fork from the forked
   // input-function stream side2 segfaults the HIP runtime in hipStreamEndCapture (ROCm 7.2, torch
   // 2.10), while eager execution of the same sequence is correct.  Four topologies, each run once:
@@ -1539,8 +1579,15 @@ int run_wgrad_side(Ctx& c, const WgradGroup& G, std::initializer_list<const floa
   // "capture fault".
   if (serial || c.s == p->side2) {
     float* slab = c.s == p->side2 ? p->P_("slab_wgrad2") : p->P_("slab_wgrad");
-    ProfScope ps(c, G.b16 ? "wgrad_b16" : "wgrad", group_flops(G));
-    GNOT_RUN(launch_group(c.p, G, slab, c.s));
+    {
+      ProfScope ps(c, G.b16 ? "wgrad_b16" : "wgrad", group_flops(G));
+      GNOT_RUN(launch_group(c.p, G, slab, c.s));
+    }
+    if (p->grad_comm_on) {
+      hipEvent_t done = next_event(p);
+      GNOT_CK(hipEventRecord(done, c.s));
+      GNOT_RUN(grad_allreduce(p, G, done));
+    }
     return GNOT_OK;
   }
   hipEvent_t fork = next_event(p);
@@ -1554,6 +1601,7 @@ int run_wgrad_side(Ctx& c, const WgradGroup& G, std::initializer_list<const floa
   hipEvent_t done = next_event(p);
   GNOT_CK(hipEventRecord(done, p->side));
   for (const float* r : reads) p->readers[r] = done;
+  if (p->grad_comm_on) GNOT_RUN(grad_allreduce(p, G, done));
   return GNOT_OK;
 }
 
@@ -1824,6 +1872,12 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
   float* dquery = p->P_("dquery");
   float* stage = p->moe_walk ? nullptr : p->P_("stage");
   p->readers.clear();
+  if (p->grad_comm_on) {                   // the comm stream joins here (a first-level fork of the caller's)
+    if (!p->comm_stream) GNOT_CK(hipStreamCreateWithFlags(&p->comm_stream, hipStreamNonBlocking));
+    hipEvent_t fork = next_event(p);
+    GNOT_CK(hipEventRecord(fork, c.s));
+    GNOT_CK(hipStreamWaitEvent(p->comm_stream, fork, 0));
+  }
   GNOT_CK(hipMemcpy2DAsync(p->P_("dout"), p->bufs["dout"].ld * 4, dout, p->out * 4, p->out * 4, P,
                            hipMemcpyDeviceToDevice, c.s));
   GNOT_CK(hipMemsetAsync(p->P_("dscore"), 0, P * p->bufs["dscore"].ld * 4, c.s));
@@ -1959,6 +2013,11 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
   hipEvent_t join = next_event(p);
   GNOT_CK(hipEventRecord(join, p->side));
   GNOT_CK(hipStreamWaitEvent(c.s, join, 0));
+  if (p->grad_comm_on) {                   // ... and summed over the ranks
+    hipEvent_t joinc = next_event(p);
+    GNOT_CK(hipEventRecord(joinc, p->comm_stream));
+    GNOT_CK(hipStreamWaitEvent(c.s, joinc, 0));
+  }
   p->readers.clear();
   p->bwd_done = true;
   return GNOT_OK;

@@ -86,6 +86,21 @@ int main(int argc, char** argv) {
   bw.dz_chain_stride = (long)NL * P * D; bw.dX = dX; bw.lddx = D; bw.dx_chain_stride = (long)P * D;
   t = time_us([&] { CK(launch_chain_bwd(bw, nullptr)); });
   std::printf("chain_bwd  MoE E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
+  if (D == 256) {   // the fused soft-MoE combine (counters zero between launches)
+    int* cnt = nullptr;
+    CK(hipMalloc(&cnt, ((P + 127) / 128) * sizeof(int)));
+    CK(hipMemset(cnt, 0, ((P + 127) / 128) * sizeof(int)));
+    float* qout = dalloc((size_t)P * D, 0.0f);
+    ChainArgs af = a, bf = bw;
+    af.base = X; af.combine = qout; af.counters = cnt;
+    bf.combine = qout; bf.counters = cnt;
+    t = time_us([&] { CK(launch_chain_fwd(af, nullptr)); });
+    std::printf("chain_fwd  MoE+combine E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
+    t = time_us([&] { CK(launch_chain_bwd(bf, nullptr)); });
+    std::printf("chain_bwd  MoE+combine E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
+    CK(hipFree(qout));
+    CK(hipFree(cnt));
+  }
   if (D == 256) {   // bf16 arithmetic mode (one operand piece)
     ChainArgs a1 = a, b1 = bw;
     a1.np = 1; b1.np = 1;
@@ -102,8 +117,22 @@ int main(int argc, char** argv) {
     std::printf("chain_fwd  b16s E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
     t = time_us([&] { CK(launch_chain_bwd(b2, nullptr)); });
     std::printf("chain_bwd  b16s E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
+    int* cnt = nullptr;
+    CK(hipMalloc(&cnt, ((P + 127) / 128) * sizeof(int)));
+    CK(hipMemset(cnt, 0, ((P + 127) / 128) * sizeof(int)));
+    float* qout = dalloc((size_t)P * D, 0.0f);
+    ChainArgs af = a2, bf = b2;
+    af.base = X; af.combine = qout; af.counters = cnt;
+    bf.combine = qout; bf.counters = cnt;
+    t = time_us([&] { CK(launch_chain_fwd(af, nullptr)); });
+    std::printf("chain_fwd  b16s+combine E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
+    t = time_us([&] { CK(launch_chain_bwd(bf, nullptr)); });
+    std::printf("chain_bwd  b16s+combine E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
+    CK(hipFree(qout));
+    CK(hipFree(cnt));
   }
 
+  if (argc > 4 && std::atoi(argv[4]) == 1) return 0;   // chains only
   for (int NO : {D, 3 * D}) {
     LinearArgs l{};
     l.nseg = 1; l.X[0] = X; l.Wp[0] = W; l.ldx = D; l.nsum = 1; l.K = D; l.bias = bias; l.Y = Y; l.ldy = NO;

@@ -355,22 +355,31 @@ __global__ void __launch_bounds__(256) pgemm_x6_kernel(const WgradJob* __restric
 // stages each value twice and splits it on the same wave that issues the MFMAs).  8 waves, two per
 // SIMD (<= 256 registers each: the accumulators are 8 32x32 blocks = 128 AGPRs), so one wave's
 // staging VALU runs beside its partner's MFMAs.
-//   staging: thread t owns feature f = t & 255 and point half h = t >> 8 of a 16-point stage, for both
-//            operands: 8 dword loads per operand (a wave-instruction reads 256 contiguous bytes of one
-//            row), then 3 bf16 pieces of 8 consecutive points = three 16-byte LDS stores.
+//   rows:    the raw fp32 rows of a 16-point stage land by LDS-DMA in a ring PRIVATE to each wave: wave w
+//            stages features 64 (w & 3) .. +63 of points 8 (w >> 2) .. +7 and brings exactly those 8 x 64
+//            values of each operand (2 wave-instructions of 1 KiB per operand), so no barrier hands them
+//            over and its slot is refilled as soon as its own reads of it have returned.  Two slots: stage
+//            s + 3 is requested while stage s is multiplied and read at the top of iteration s + 2 (the
+//            HBM latency of the row loads, the kernel's first limiter, DESIGN.md section 5.2, gets two
+//            iterations instead of one, and the raw rows in flight hold no registers).
+//   staging: thread t owns feature f = t & 255 and point half h = t >> 8 of a stage, for both operands:
+//            mask, column sum, GELU, then 3 bf16 pieces of 8 consecutive points = three 16-byte LDS stores.
 //   LDS:     per (buffer, operand, piece) a fragment-order image of 8 row blocks x 64 lanes x 16 B:
 //            lane (r, h) of block rb holds rows 32 rb + r, points 8h .. 8h+7 -- the A/B operand layout of
 //            v_mfma_f32_32x32x16_bf16, so fragment reads are contiguous 1 KiB ds_read_b128.
 //   MFMA:    wave (wr, wc) computes rows [128 wr, +128) x cols [64 wc, +64): 4 x 2 blocks, six order <= 2
 //            piece products each (smallest first), one accumulator per block.
-// Double-buffered: stage s+1 is split into the other buffer while stage s is multiplied; its rows were
-// loaded one stage earlier.  Partials go to the same slab layout as pgemm_kernel (128-tiles).
+// Double-buffered fragment images: stage s+1 is split into the other buffer while stage s is multiplied.
+// Partials go to the same slab layout as pgemm_kernel (128-tiles).
 constexpr int kWStage = 16;
 constexpr int kWThreads = 512;
 constexpr int kWPiece = 8 * 64;                  // u32x4 per (operand, piece) image
 // one stage buffer: A pieces 0..NP-1 | B pieces 0..NP-1 (NP = 3: bf16x6, 1: bf16 mode)
 constexpr int w_buf(int np) { return 2 * np * kWPiece; }
-constexpr size_t w_lds_bytes(int np) { return 2 * (size_t)w_buf(np) * 16; }   // 96 KiB at NP = 3
+constexpr int kWRawSlot = 2 * 2 * 64;            // u32x4 per wave-private raw slot: 2 operands x 2 KiB
+constexpr int kWRawSlots = 2;
+// LDS: two fragment buffers | 8 waves x 2 raw slots (96 + 64 = 160 KiB at NP = 3)
+constexpr size_t w_lds_bytes(int np) { return (2 * (size_t)w_buf(np) + 8 * kWRawSlots * kWRawSlot) * 16; }
 
 GNOT_DEV void x6_mfma6(const u32x4 (&a)[3], const u32x4 (&b)[3], f32x16& c) {
 #define GNOT_MFMA32(X, Y) \
@@ -389,9 +398,14 @@ GNOT_DEV void mfma_np(const u32x4 (&a)[NP], const u32x4 (&b)[NP], f32x16& c) {
   else c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[0]), __builtin_bit_cast(bf16x8, b[0]), c, 0, 0, 0);
 }
 
-// the wide kernel's row loads (default cache policy: nt measured within noise)
-GNOT_DEV float wrow_load(rsrc_t r, int voff, int soff) {
-  return u2f(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+// one dword of a wave-private raw slot (inline asm: the compiler does not order it against the LDS-DMA
+// still in flight to the OTHER slot; the caller's counted vmcnt already retired this slot's DMA, and a
+// later `s_waitcnt lgkmcnt(0)` that names the register makes the value valid)
+template <int OFF>
+GNOT_DEV float lds_read_b32_off(unsigned addr) {
+  float v;
+  asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "n"(OFF) : "memory");
+  return v;
 }
 
 template <int NP = 3>
@@ -400,17 +414,17 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
                                                               float* __restrict__ slab) {
   extern __shared__ __attribute__((aligned(16))) u32x4 wl[];
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int j = find_job(prefix, njobs, blockIdx.x);
   const WgradJob J = jobs[j];
   const int split = blockIdx.x - prefix[j];
   const int chunk = ((J.P + J.splits - 1) / J.splits + kWStage - 1) / kWStage * kWStage;
   const long pb = (long)split * chunk;
   const long pe = min((long)J.P, pb + chunk);
+  const int nst = pe > pb ? (int)((pe - pb + kWStage - 1) / kWStage) : 0;
   // staging role (the point half hh is wave-uniform: waves 0-3 / 4-7)
   const int f = tid & 255, hh = tid >> 8;
   const bool fa = f < J.out, fb = f < J.in;
-  const int fca = min(f, J.out - 1), fcb = min(f, J.in - 1);
   const int sdst = (f >> 5) * 64 + (f & 31) + 32 * hh;
   // MFMA role
   const int wr = wave >> 2, wc = wave & 3;
@@ -425,35 +439,54 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{};
   float dbacc = 0.f;
-  struct Raw {
-    float a[8], b[8];
-  };
-  // buffer loads from resources based at the split's first row (64-bit base, so the 32-bit offsets span
-  // one split: finish_group bounds a split's rows x pitch below 2^31 bytes): rows past the split read 0
-  // (only the last split ends inside a stage: chunks are whole stages; the loads one stage past a split's
-  // end are never staged), columns past out / in are masked; the row offset is wave-uniform (SGPR)
+  float ra_raw[8], rb_raw[8];                      // this thread's 8 points of the stage being staged
+  // buffer resources based at the split's first row (64-bit base, so the 32-bit offsets span one split:
+  // finish_group bounds a split's rows x pitch below 2^31 bytes): rows past the split read 0 (only the
+  // last split ends inside a stage; the DMAs of stages past a split's end bring zeros nobody reads);
+  // columns past out / in (inside the row pitch, which is a multiple of 4) are masked at staging
   const long nsp = pe > pb ? pe - pb : 0;
   const rsrc_t rA = make_rsrc(J.dz + pb * J.lddz, (unsigned)(nsp * J.lddz * 4));
   const rsrc_t rB = make_rsrc(J.x + pb * J.ldx, (unsigned)(nsp * J.ldx * 4));
-  const int voA = fca * 4, voB = fcb * 4;
-  const int hw = __builtin_amdgcn_readfirstlane(hh);
-  auto load = [&](Raw& R, long p0) {
-    const unsigned pr = (unsigned)(p0 - pb + 8 * hw);
-    // raw values only: any arithmetic on them here would make the wave wait for the load now
+  // DMA lane role: instruction i of operand o brings points 4 i + (lane >> 4) of the wave's half, features
+  // 64 (wave & 3) + 4 (lane & 15) .. +3; in the slot, point k of the half is the 256-byte row k (64 floats)
+  const int fcol = 64 * (wave & 3) + 4 * (lane & 15);
+  const int dvA = ((lane >> 4) * (int)J.lddz + fcol) * 4, dvB = ((lane >> 4) * (int)J.ldx + fcol) * 4;
+  u32x4* const raw = wl + 2 * w_buf(NP) + wave * kWRawSlots * kWRawSlot;
+  auto raw_dma = [&](int st) __attribute__((always_inline)) {
+    u32x4* dst = raw + (st & 1) * kWRawSlot;
+    const unsigned p0 = (unsigned)(st * kWStage + 8 * (wave >> 2));
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      R.a[k] = wrow_load(rA, voA, (int)((pr + k) * (unsigned)J.lddz * 4u));
-      R.b[k] = wrow_load(rB, voB, (int)((pr + k) * (unsigned)J.ldx * 4u));
+    for (int i = 0; i < 2; ++i) {
+      dma16(rA, dst + i * 64, dvA, (int)((p0 + 4 * i) * (unsigned)J.lddz * 4u));
+      dma16(rB, dst + 128 + i * 64, dvB, (int)((p0 + 4 * i) * (unsigned)J.ldx * 4u));
     }
+  };
+  const unsigned raw_addr = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) u32x4*)raw + 4u * lane;
+  // this thread's 8 points of stage st (its slot's DMAs retired by the caller's counted wait)
+  auto raw_read = [&](int st) __attribute__((always_inline)) {
+    const unsigned a = raw_addr + (unsigned)((st & 1) * kWRawSlot * 16);
+    ra_raw[0] = lds_read_b32_off<0>(a);    rb_raw[0] = lds_read_b32_off<2048>(a);
+    ra_raw[1] = lds_read_b32_off<256>(a);  rb_raw[1] = lds_read_b32_off<2304>(a);
+    ra_raw[2] = lds_read_b32_off<512>(a);  rb_raw[2] = lds_read_b32_off<2560>(a);
+    ra_raw[3] = lds_read_b32_off<768>(a);  rb_raw[3] = lds_read_b32_off<2816>(a);
+    ra_raw[4] = lds_read_b32_off<1024>(a); rb_raw[4] = lds_read_b32_off<3072>(a);
+    ra_raw[5] = lds_read_b32_off<1280>(a); rb_raw[5] = lds_read_b32_off<3328>(a);
+    ra_raw[6] = lds_read_b32_off<1536>(a); rb_raw[6] = lds_read_b32_off<3584>(a);
+    ra_raw[7] = lds_read_b32_off<1792>(a); rb_raw[7] = lds_read_b32_off<3840>(a);
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(ra_raw[0]), "+v"(ra_raw[1]), "+v"(ra_raw[2]), "+v"(ra_raw[3]), "+v"(ra_raw[4]),
+                   "+v"(ra_raw[5]), "+v"(ra_raw[6]), "+v"(ra_raw[7]), "+v"(rb_raw[0]), "+v"(rb_raw[1]),
+                   "+v"(rb_raw[2]), "+v"(rb_raw[3]), "+v"(rb_raw[4]), "+v"(rb_raw[5]), "+v"(rb_raw[6]),
+                   "+v"(rb_raw[7])::"memory");
   };
   // split + LDS store of the staged rows; gel is uniform per workgroup: one branch around the whole
   // stage (not per element), so each variant is one straight-line block the scheduler can interleave
-  auto stage_v = [&](int buf, const Raw& R, auto GEL) {
+  auto stage_v = [&](int buf, auto GEL) {
     float ra[8], vb[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      ra[k] = fa ? R.a[k] : 0.f;                  // columns past out / in
-      const float b = fb ? R.b[k] : 0.f;
+      ra[k] = fa ? ra_raw[k] : 0.f;               // columns past out / in
+      const float b = fb ? rb_raw[k] : 0.f;
       dbacc += ra[k];
       vb[k] = decltype(GEL)::value ? gelu(b) : b;
     }
@@ -467,9 +500,9 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
       base[(NP + q) * kWPiece + sdst] = pq[q];
     }
   };
-  auto stage = [&](int buf, const Raw& R) {
-    if (gel) stage_v(buf, R, std::true_type{});
-    else stage_v(buf, R, std::false_type{});
+  auto stage = [&](int buf) {
+    if (gel) stage_v(buf, std::true_type{});
+    else stage_v(buf, std::false_type{});
   };
   auto compute = [&](int buf) {
     const u32x4* A = wl + buf * w_buf(NP);
@@ -479,11 +512,64 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
     for (int jb = 0; jb < 2; ++jb)
 #pragma unroll
       for (int q = 0; q < NP; ++q) bf[jb][q] = Bm[q * kWPiece + (wc * 2 + jb) * 64 + lane];
-    if (full) {
-      // row-block fragments one block ahead (two sets live: the register budget of two waves per SIMD)
-      u32x4 af[2][NP];
+#pragma unroll
+    for (int ib = 0; ib < 4; ++ib) {
+      if (ib >= nrb) break;
+      u32x4 af[NP];
+#pragma unroll
+      for (int q = 0; q < NP; ++q) af[q] = A[q * kWPiece + (wr * 4 + ib) * 64 + lane];
+      if (ncb > 0) mfma_np<NP>(af, bf[0], acc[ib][0]);
+      if (ncb > 1) mfma_np<NP>(af, bf[1], acc[ib][1]);
+    }
+  };
+  // the LDS hand-off of the fragment images: their stores retired, then the workgroup barrier (no vmcnt:
+  // the raw DMAs stay in flight across it)
+  auto lds_barrier = []() __attribute__((always_inline)) { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+
+  // The staging of stage s+1 (GELU, split, LDS stores) is interleaved instruction by instruction with the
+  // MFMAs of stage s on the SAME wave, so the VALU issues in the MFMA shadows instead of in a separate
+  // phase that both waves of a SIMD reach together after every barrier (full 256 x 256 tiles; edge tiles
+  // take the plain double-buffered loop)
+  if (nst > 0) {
+    // prologue: stages 0 and 1 requested; stage 0 read (its slot then refilled with stage 2) and staged
+    raw_dma(0);
+    raw_dma(1);
+    c2_wait_vm<4>();
+    raw_read(0);
+    raw_dma(2);
+    stage(0);
+    lds_barrier();
+    int buf = 0;
+    // MASK: columns past out / in exist (the fa / fb selects); jobs with out = in = 256 skip them
+    auto fused = [&](int b, auto GEL, auto MASK) {
+      const u32x4* A = wl + b * w_buf(NP);
+      const u32x4* Bm = A + NP * kWPiece;
+      u32x4 bf[2][NP], af[2][NP], pa[NP], pq[NP];
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+        for (int q = 0; q < NP; ++q) bf[jb][q] = Bm[q * kWPiece + (wc * 2 + jb) * 64 + lane];
 #pragma unroll
       for (int q = 0; q < NP; ++q) af[0][q] = A[q * kWPiece + (wr * 4) * 64 + lane];
+      float ra[8], vb[8];
+      // after each six-MFMA group (one 32 x 32 block) one point's staging (mask, column sum, GELU; every
+      // second point the split of the pair just finished); sched_barrier pins the order, so each wave
+      // alternates MFMA groups and VALU chunks and the two waves of a SIMD fill each other's gaps
+      auto chunk = [&](int k) {
+        ra[k] = (!decltype(MASK)::value || fa) ? ra_raw[k] : 0.f;
+        dbacc += ra[k];
+        const float bv = (!decltype(MASK)::value || fb) ? rb_raw[k] : 0.f;
+        vb[k] = decltype(GEL)::value ? gelu(bv) : bv;
+        // pin the chunk's results here: IR-level sinking would otherwise move the whole staging
+        // next to its LDS stores after the last MFMA group (sched_barrier only binds the scheduler)
+        asm volatile("" : "+v"(ra[k]), "+v"(vb[k]), "+v"(dbacc));
+        if (k & 1) {
+          split2_np<NP>(ra[k - 1], ra[k], pa, k >> 1);
+          split2_np<NP>(vb[k - 1], vb[k], pq, k >> 1);
+#pragma unroll
+          for (int q = 0; q < NP; ++q) asm volatile("" : "+v"(pa[q][k >> 1]), "+v"(pq[q][k >> 1]));
+        }
+      };
 #pragma unroll
       for (int ib = 0; ib < 4; ++ib) {
         if (ib + 1 < 4) {
@@ -491,125 +577,55 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
           for (int q = 0; q < NP; ++q) af[(ib + 1) & 1][q] = A[q * kWPiece + (wr * 4 + ib + 1) * 64 + lane];
         }
         mfma_np<NP>(af[ib & 1], bf[0], acc[ib][0]);
+        __builtin_amdgcn_sched_barrier(0);
+        chunk(2 * ib);
+        __builtin_amdgcn_sched_barrier(0);
         mfma_np<NP>(af[ib & 1], bf[1], acc[ib][1]);
         __builtin_amdgcn_sched_barrier(0);
+        chunk(2 * ib + 1);
+        __builtin_amdgcn_sched_barrier(0);
       }
-    } else {
+      u32x4* base = wl + (b ^ 1) * w_buf(NP);
 #pragma unroll
-      for (int ib = 0; ib < 4; ++ib) {
-        if (ib >= nrb) break;
-        u32x4 af[NP];
-#pragma unroll
-        for (int q = 0; q < NP; ++q) af[q] = A[q * kWPiece + (wr * 4 + ib) * 64 + lane];
-        if (ncb > 0) mfma_np<NP>(af, bf[0], acc[ib][0]);
-        if (ncb > 1) mfma_np<NP>(af, bf[1], acc[ib][1]);
+      for (int q = 0; q < NP; ++q) {
+        base[q * kWPiece + sdst] = pa[q];
+        base[(NP + q) * kWPiece + sdst] = pq[q];
       }
-    }
-  };
-
-  // The staging of stage s+1 (GELU, split, LDS stores) and the row loads of stage s+2 are interleaved
-  // instruction by instruction with the MFMAs of stage s on the SAME wave, so the VALU issues in the MFMA
-  // shadows instead of in a separate phase that both waves of a SIMD reach together after every barrier
-  // (full 256 x 256 tiles; edge tiles take the plain double-buffered loop)
-  {
-    if (pb >= pe) {
-      // empty split: the partials below are zero
-    } else {
-      Raw R;
-      load(R, pb);
-      stage(0, R);
-      load(R, pb + kWStage);
-      __syncthreads();
-      int buf = 0;
-      long p0 = pb;
-      // compute(buf) | stage(buf ^ 1, R) | load(R, pn) as ONE program order: after each six-MFMA
-      // group (one 32 x 32 block) comes one point's staging (mask, column sum, GELU; every second
-      // point the split of the pair just finished), then that point's row loads for stage pn.
-      // sched_barrier pins the order, so each wave alternates MFMA groups and VALU chunks and the two
-      // waves of a SIMD fill each other's gaps.
-      // MASK: columns past out / in exist (the fa / fb selects); jobs with out = in = 256 skip them
-      auto fused = [&](int b, long pn, auto GEL, auto MASK) {
-        const u32x4* A = wl + b * w_buf(NP);
-        const u32x4* Bm = A + NP * kWPiece;
-        u32x4 bf[2][NP], af[2][NP], pa[NP], pq[NP];
-#pragma unroll
-        for (int jb = 0; jb < 2; ++jb)
-#pragma unroll
-          for (int q = 0; q < NP; ++q) bf[jb][q] = Bm[q * kWPiece + (wc * 2 + jb) * 64 + lane];
-#pragma unroll
-        for (int q = 0; q < NP; ++q) af[0][q] = A[q * kWPiece + (wr * 4) * 64 + lane];
-        float ra[8], vb[8];
-        const unsigned pr = (unsigned)(pn - pb + 8 * hw);
-        auto chunk = [&](int k) {
-          ra[k] = (!decltype(MASK)::value || fa) ? R.a[k] : 0.f;
-          dbacc += ra[k];
-          const float bv = (!decltype(MASK)::value || fb) ? R.b[k] : 0.f;
-          vb[k] = decltype(GEL)::value ? gelu(bv) : bv;
-          // pin the chunk's results here: IR-level sinking would otherwise move the whole staging
-          // next to its LDS stores after the last MFMA group (sched_barrier only binds the scheduler)
-          asm volatile("" : "+v"(ra[k]), "+v"(vb[k]), "+v"(dbacc));
-          if (k & 1) {
-            split2_np<NP>(ra[k - 1], ra[k], pa, k >> 1);
-            split2_np<NP>(vb[k - 1], vb[k], pq, k >> 1);
-#pragma unroll
-            for (int q = 0; q < NP; ++q) asm volatile("" : "+v"(pa[q][k >> 1]), "+v"(pq[q][k >> 1]));
-            // the pair's row loads for stage pn only after its split: the raw registers are then dead
-            // and are reloaded in place (loading them earlier forces a copy of every raw value)
-#pragma unroll
-            for (int kk = k - 1; kk <= k; ++kk) {
-              R.a[kk] = wrow_load(rA, voA, (int)((pr + kk) * (unsigned)J.lddz * 4u));
-              R.b[kk] = wrow_load(rB, voB, (int)((pr + kk) * (unsigned)J.ldx * 4u));
-            }
-          }
-        };
-#pragma unroll
-        for (int ib = 0; ib < 4; ++ib) {
-          if (ib + 1 < 4) {
-#pragma unroll
-            for (int q = 0; q < NP; ++q) af[(ib + 1) & 1][q] = A[q * kWPiece + (wr * 4 + ib + 1) * 64 + lane];
-          }
-          mfma_np<NP>(af[ib & 1], bf[0], acc[ib][0]);
-          __builtin_amdgcn_sched_barrier(0);
-          chunk(2 * ib);
-          __builtin_amdgcn_sched_barrier(0);
-          mfma_np<NP>(af[ib & 1], bf[1], acc[ib][1]);
-          __builtin_amdgcn_sched_barrier(0);
-          chunk(2 * ib + 1);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        u32x4* base = wl + (b ^ 1) * w_buf(NP);
-#pragma unroll
-        for (int q = 0; q < NP; ++q) {
-          base[q * kWPiece + sdst] = pa[q];
-          base[(NP + q) * kWPiece + sdst] = pq[q];
-        }
-      };
-      auto run = [&](auto GEL, auto MASK) {
-        for (; p0 + kWStage < pe; p0 += kWStage) {
-          fused(buf, p0 + 2 * kWStage, GEL, MASK);
-          __syncthreads();
-          buf ^= 1;
-        }
-      };
-      if (full) {
-        if (J.out >= 256 && J.in >= 256) {
-          if (gel) run(std::true_type{}, std::false_type{});
-          else run(std::false_type{}, std::false_type{});
-        } else {
-          if (gel) run(std::true_type{}, std::true_type{});
-          else run(std::false_type{}, std::true_type{});
-        }
+    };
+    // iteration s: stage s + 1's rows (the wait leaves stage s + 2's four DMAs in flight) are read, their
+    // slot refilled with stage s + 3, and staged while stage s is multiplied
+    auto run = [&](auto GEL, auto MASK) {
+      for (int s = 0; s + 1 < nst; ++s) {
+        c2_wait_vm<4>();
+        raw_read(s + 1);
+        raw_dma(s + 3);
+        fused(buf, GEL, MASK);
+        lds_barrier();
+        buf ^= 1;
+      }
+    };
+    if (full) {
+      if (J.out >= 256 && J.in >= 256) {
+        if (gel) run(std::true_type{}, std::false_type{});
+        else run(std::false_type{}, std::false_type{});
       } else {
-        for (; p0 + kWStage < pe; p0 += kWStage) {
-          compute(buf);
-          stage(buf ^ 1, R);
-          load(R, p0 + 2 * kWStage);
-          __syncthreads();
-          buf ^= 1;
-        }
+        if (gel) run(std::true_type{}, std::true_type{});
+        else run(std::false_type{}, std::true_type{});
       }
-      compute(buf);   // the last stage
+    } else {
+      for (int s = 0; s + 1 < nst; ++s) {
+        c2_wait_vm<4>();
+        raw_read(s + 1);
+        raw_dma(s + 3);
+        compute(buf);
+        stage(buf ^ 1);
+        lds_barrier();
+        buf ^= 1;
+      }
     }
+    compute(buf);   // the last stage
+    // the DMAs of the two stages past the end (zeros) land before the workgroup's LDS is released
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
 
   // partials -> slab [split][128-tile][128 x (128 + 1)] (the pgemm_kernel layout)

@@ -142,6 +142,11 @@ template <int N>
 GNOT_DEV void c2_sync() {
   asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
 }
+// counted wait without a barrier (the wave's own LDS-DMA)
+template <int N>
+GNOT_DEV void c2_wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 GNOT_DEV void c2_sync_n(int n) {   // n is wave-uniform and small
   switch (n) {
     case 1: c2_sync<1>(); break;

@@ -28,7 +28,7 @@ EXPORTS = [
     "gnot_plan_bind_workspace", "gnot_plan_bind_workspace_async", "gnot_plan_set_moe_recompute", "gnot_plan_set_precision",
     "gnot_plan_set_input_grads", "gnot_input_grads", "gnot_plan_grad_offsets", "gnot_pack_weights", "gnot_forward",
     "gnot_backward", "gnot_profile_enable", "gnot_profile_read", "gnot_debug_buffer", "gnot_last_error",
-    "gnot_version", "gnot_plan_set_shard", "gnot_shard_range", "gnot_shard_exchange",
+    "gnot_version", "gnot_plan_set_shard", "gnot_plan_set_grad_comm", "gnot_shard_range", "gnot_shard_exchange",
     "gnot_rel_l2_work_floats", "gnot_rel_l2_loss", "gnot_adamw_step",
 ]
 
@@ -78,6 +78,7 @@ def _declare(lib):
                                       ctypes.POINTER(ctypes.c_double)]
     lib.gnot_debug_buffer.argtypes = [P, ctypes.c_char_p, ctypes.POINTER(P), ctypes.POINTER(i64)]
     lib.gnot_plan_set_shard.argtypes = [P, i32, i32, i32, ctypes.POINTER(i64), ctypes.POINTER(GnotComm)]
+    lib.gnot_plan_set_grad_comm.argtypes = [P, ctypes.POINTER(GnotComm)]
     lib.gnot_shard_range.argtypes = [i64, i32, i32, ctypes.POINTER(i64), ctypes.POINTER(i64)]
     lib.gnot_shard_exchange.argtypes = [i32, ctypes.POINTER(i64), i32, i32, i32, i32, ctypes.POINTER(i64),
                                         ctypes.POINTER(i64), ctypes.POINTER(i64), i64, ctypes.POINTER(i64)]

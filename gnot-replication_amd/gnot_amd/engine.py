@@ -41,6 +41,7 @@ class Engine:
         self.grad_flat = None      # the flat copy of the arena handed to autograd by the last backward
         self.param_grads = True    # False: no .grad tensors; grad_flat IS the arena (FlatAdamW reads it)
         self.comm = None           # parallel.PointShardComm when points are sharded over ranks
+        self.grad_comm = None      # parallel.PointShardComm: gradients summed over ranks inside the backward
         self.moe_recompute = False # re-run each MoE call's expert forward in the backward (memory option)
         self.bf16 = False          # bf16 arithmetic mode of the d = 256 MFMA kernels (gnot_plan_set_precision)
         self.input_grads = False   # also differentiate x, theta, input functions (gnot_plan_set_input_grads)
@@ -73,7 +74,7 @@ class Engine:
         self._bind_params()
         geom = (tuple(x_off), tuple(tuple(o) for o in fn_offs), bool(training),
                 tuple(n_global) if n_global is not None else None, bool(self.moe_recompute), bool(self.bf16),
-                bool(self.input_grads) and bool(training))
+                bool(self.input_grads) and bool(training), id(self.grad_comm))
         if geom == self.geom:
             return
         B = len(x_off) - 1
@@ -105,6 +106,11 @@ class Engine:
         _lib.check(self.lib.gnot_plan_bind_workspace_async(self.plan, self.ws.data_ptr(), self.ws.numel(), s))
         if self.comm is not None:
             self.comm.ws = self.ws
+        if self.grad_comm is not None:
+            self.grad_comm.ws = self.ws
+            _lib.check(self.lib.gnot_plan_set_grad_comm(self.plan, ctypes.byref(self.grad_comm.struct)))
+        else:
+            _lib.check(self.lib.gnot_plan_set_grad_comm(self.plan, None))
         self.geom = geom
         self.grad_views = None
         self.grad_arena = None

@@ -153,6 +153,7 @@ class GNOT(nn.Module):
                          n_input_functions=n_input_functions)
         self._engine = None
         self._comm = None          # parallel.PointShardComm (set_point_shard); survives engine rebuilds
+        self._grad_comm = None     # parallel.PointShardComm (set_grad_allreduce)
         self._moe_recompute = False
         self._bf16 = False
 
@@ -169,6 +170,7 @@ class GNOT(nn.Module):
         if self._engine is None:
             self._engine = Engine(self._cfg, self.linears())
             self._engine.comm = self._comm
+            self._engine.grad_comm = self._grad_comm
             self._engine.moe_recompute = self._moe_recompute
             self._engine.bf16 = self._bf16
         return self._engine
@@ -225,6 +227,15 @@ class GNOT(nn.Module):
         None to switch sharding off.  forward_packed then takes this rank's slices plus n_global."""
         self._comm = comm
         self.engine().comm = comm
+        self.engine().geom = None
+
+    def set_grad_allreduce(self, comm):
+        """Sum the parameter gradients over the ranks of `comm` (gnot_amd.parallel.PointShardComm) INSIDE
+        the backward, one collective per weight-gradient group as soon as the group is written, overlapped
+        with the rest of the backward (gnot_plan_set_grad_comm); None switches it off (the caller reduces
+        the gradients itself, e.g. one all-reduce of engine().grad_flat)."""
+        self._grad_comm = comm
+        self.engine().grad_comm = comm
         self.engine().geom = None
 
     def forward_packed(self, x, x_off, theta, fns=(), fn_offs=(), n_global=None):

@@ -1,6 +1,8 @@
 """Multi-GPU host logic of the GNOT hot path.  One process per GPU.
 
-Two modes, both with ONE gradient all-reduce of the flat gradient buffer per step:
+Two modes; in both the parameter gradients are summed over the ranks, either by one all-reduce of the
+flat gradient buffer after the backward or -- `GNOT.set_grad_allreduce` -- group by group inside the
+backward, overlapped with it (gnot_plan_set_grad_comm):
 
 * sample data parallel (small meshes, BASELINE configs[1]/[4]): every rank owns whole meshes
   (`lpt_partition` balances them by point count); gradients are averaged / summed.
@@ -70,7 +72,8 @@ def lpt_partition(sizes, world):
 
 
 class PointShardComm:
-    """gnot_comm backed by a torch.distributed process group.
+    """gnot_comm backed by a torch.distributed process group: the point-shard exchanges
+    (GNOT.set_point_shard) and the overlapped gradient all-reduce (GNOT.set_grad_allreduce).
 
     The engine hands over raw pointers into its workspace; they are wrapped as float32 views of the
     workspace tensor (no copies).  With RCCL (`nccl` backend) every collective is issued on the

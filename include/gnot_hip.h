@@ -161,6 +161,16 @@ typedef struct gnot_comm {
                    const int64_t* recv_counts, void* stream);
 } gnot_comm;
 
+/* Gradient all-reduce overlapped with the backward (data-parallel training over ranks: sample-DP, or the
+ * parameter gradients of a point-sharded batch).  With comm != NULL, gnot_backward sums every weight-
+ * gradient group's contiguous (dW, db) ranges of the gradient arena over the ranks (comm->allreduce_sum,
+ * in place) on a stream of its own as soon as that group's kernels have written them, and joins that
+ * stream into `stream` before it returns -- the arena then holds the rank sums.  NULL switches it off
+ * (the caller reduces the arena itself).  `comm` is copied; only allreduce_sum is used.  No reference
+ * counterpart (main.py:27 is single-device); SURVEY.md section 5 "weight-grad all-reduce overlapped with
+ * backward". */
+int gnot_plan_set_grad_comm(gnot_plan* plan, const gnot_comm* comm);
+
 /* Declare the rank's shard of the next batch: n_global[b] = points of sample b over all ranks.
  * Call before gnot_plan_set_batch, whose x_off then gives the LOCAL slices (validated against
  * gnot_shard_range).  world == 1 (or comm == NULL) switches sharding off.  `comm` is copied. */

@@ -8,6 +8,8 @@
 #   bench[:<bench.py args>]          one bench line -> <tag>_bench<n>.json
 #   prof[:<bench.py args>]           rocprofv3 --kernel-trace --stats of a short bench run -> <tag>_prof<n>/
 #   mb[:<microbench args>]           the kernel microbenchmark (lib/microbench)
+#   mbx:<suffix>+<args>              an experimental build of it (lib/microbench_<suffix>)
+#   dist:<nproc>+<bench args>        bench.py over <nproc> gloo ranks sharing cuda:0 (multi-GPU rehearsal)
 set -o pipefail
 TAG=${1:?tag}; shift
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -45,6 +47,17 @@ for step in "$@"; do
       rc=$?; tail -3 $out.log ;;
     mb)
       timeout -k 10 300 gnot-replication_amd/lib/microbench $arg > $out.log 2>&1
+      rc=$?; tail -30 $out.log ;;
+    dist)  # dist:<nproc>+<bench args>: multi-process rehearsal on the one GPU (gloo, every rank on cuda:0)
+      set -- $arg
+      np=$1; shift
+      GNOT_BENCH_BACKEND=gloo GNOT_BENCH_ONE_GPU=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node $np --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus $np "$@" > $out.json 2> $out.err
+      rc=$?; tail -c 1200 $out.json; [ $rc -eq 0 ] || tail -30 $out.err ;;
+    mbx)   # an experimental microbench build: mbx:<suffix>+<args> runs lib/microbench_<suffix>
+      set -- $arg
+      sfx=$1; shift
+      timeout -k 10 300 gnot-replication_amd/lib/microbench_$sfx "$@" > $out.log 2>&1
       rc=$?; tail -30 $out.log ;;
     *) echo "unknown step $kind" >&2; exit 2 ;;
   esac

@@ -39,3 +39,31 @@ def test_recompute_matches_saved_activations_bitwise(d, E, I, prec):
     assert torch.equal(o0, o1) and torch.equal(o0, o2)
     for a, b, c in zip(g0, g1, g2):
         assert torch.equal(a, b) and torch.equal(a, c)
+
+
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_serial_weight_gradients_match_side_stream_bitwise(prec, monkeypatch):
+    """GNOT_SERIAL_WGRAD=1 (read when the plan is created): every weight-gradient group on the caller's
+    stream instead of the side stream -- the same kernels in the same order per group, so outputs and
+    gradients are bitwise those of the overlapped default (configs[2] widths, input functions)."""
+    from gnot_amd import GNOT
+    dev = torch.device("cuda")
+    g = torch.Generator(device="cpu").manual_seed(21)
+    x_off = [0, 1700, 2300]
+    x = torch.rand(x_off[-1], 3, generator=g).to(dev)
+    theta = torch.rand(2, 1, generator=g).to(dev)
+    fns = [torch.rand(300, 3, generator=g).to(dev)]
+    tgt = torch.randn(x_off[-1], 1, generator=g).to(dev)
+    res = []
+    for serial in ("0", "1"):
+        monkeypatch.setenv("GNOT_SERIAL_WGRAD", serial)
+        torch.manual_seed(7)
+        model = GNOT(3, 1, 3, 1, 2, 256, 4, 256, 256, 8, 8, 1).to(dev)
+        model.set_precision(prec)
+        out = model.forward_packed(x, x_off, theta, fns, [[0, 120, 300]])
+        ((out - tgt) ** 2).sum().backward()
+        torch.cuda.synchronize()
+        res.append((out.detach().clone(), [p.grad.detach().clone() for p in model.parameters()]))
+    (o0, g0), (o1, g1) = res
+    assert torch.equal(o0, o1)
+    assert all(torch.equal(a, b) for a, b in zip(g0, g1))
