@@ -60,24 +60,40 @@ struct C2Lds {
 
 // ------------------------------------------------------------------------------ expert grid and combine
 // Workgroup -> (128-point block, expert).  Workgroups are dealt round-robin over the 8 XCDs (w and w + 8
-// share one, MI355X_MICROARCH.md "Workgroup dispatch"), so the E experts of a block are given ids
-// w = 8 (E (b / 8) + e) + b % 8: they run at the same time on CUs of ONE XCD, read the block's input rows
-// (forward: the MoE input; backward: dquery, the scores) once from HBM into that XCD's L2, and the fused
-// combine below reads their stage rows while they are fresh.  Speed only: nothing depends on placement.
-// The walk form (one workgroup per block, all experts) and single chains keep blockIdx.x.
-GNOT_DEV void c2_grid_pos(int E, bool grouped, int& blk, int& e) {
-  if (!grouped || gridDim.y > 1) {
+// share one, MI355X_MICROARCH.md "Workgroup dispatch"); speed only, nothing depends on placement.
+//   mode 1 "grouped": w = 8 (E (b / 8) + e) + b % 8 -- the E experts of a block run at the same time on
+//          ONE XCD and read the block's input rows (forward: the MoE input; backward: dquery, the scores)
+//          once from HBM into its L2; every XCD streams all E experts' weights;
+//   mode 2 "expert per XCD" (E divides 8): XCD x runs expert x % E only, so its L2 holds one expert's
+//          weight images, and the blocks advance at the same pace on every XCD, so the E reads of a
+//          block's input rows fall together in the shared Infinity Cache;
+//   mode 0: blockIdx.x = block, blockIdx.y = expert (the walk form and single chains always).
+GNOT_DEV void c2_grid_pos(int E, int mode, int& blk, int& e) {
+  if (mode == 0 || gridDim.y > 1) {
     blk = (int)blockIdx.x;
     e = (int)blockIdx.y;
     return;
   }
-  const int w = (int)blockIdx.x, s = w >> 3;
+  const int w = (int)blockIdx.x, x = w & 7, s = w >> 3;
+  if (mode == 2) {
+    e = x % E;
+    blk = s * (8 / E) + x / E;
+    return;
+  }
   e = s % E;
-  blk = (s / E) * 8 + (w & 7);
+  blk = (s / E) * 8 + x;
 }
-// grid of the expert grid: ceil(blocks / 8) * 8 * E workgroups (the ids past the last block exit at once)
-inline unsigned c2_grid_size(int nblocks, int E, bool grouped) {
-  return grouped ? (unsigned)((nblocks + 7) / 8 * 8) * (unsigned)E : (unsigned)nblocks;
+// the grid mode of an expert grid of E chains (env GNOT_C2_GRID: A/B runs)
+static int c2_grid_mode(int E) {
+  static const int env = std::getenv("GNOT_C2_GRID") ? std::atoi(std::getenv("GNOT_C2_GRID")) : -1;
+  if (E <= 1) return 0;
+  if (env >= 0) return (env == 2 && 8 % E != 0) ? 1 : env;
+  return 8 % E == 0 ? 2 : 1;
+}
+// 1-D grid of the grid modes 1 / 2 (the ids past the last block exit at once)
+inline unsigned c2_grid_size(int nblocks, int E, int mode) {
+  if (mode == 2) return (unsigned)((nblocks + 8 / E - 1) / (8 / E)) * 8u;
+  return (unsigned)((nblocks + 7) / 8 * 8) * (unsigned)E;
 }
 
 // OT point-form tiles of this lane's row (rows of 256 fp32, voff = row-in-block * 1 KiB + 16 B * g) stored
@@ -90,6 +106,26 @@ GNOT_DEV void store_rows_sc1(const float (&v)[OT][4], rsrc_t r, int voff) {
                                            r, voff + 64 * T, 0, kCpolSc1);
 }
 
+// the same tiles as RNE bf16 at their pair-interleaved positions (rowoff = row-in-block * 512 B), write-through
+template <int KT>
+GNOT_DEV void store_rows_b16_sc1(const float (&a)[KT][4], rsrc_t r, int rowoff, int lane) {
+  const int g = lane >> 4;
+#pragma unroll
+  for (int t = 0; t < KT / 2; ++t)
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{pk_bf16(a[2 * t][0], a[2 * t][1]), pk_bf16(a[2 * t][2], a[2 * t][3]),
+                                                 pk_bf16(a[2 * t + 1][0], a[2 * t + 1][1]),
+                                                 pk_bf16(a[2 * t + 1][2], a[2 * t + 1][3])},
+                                           r, rowoff + (t * 4 + g) * 16, 0, kCpolSc1);
+}
+// in place: each value rounded to bf16 (RNE, the bits store_rows_b16_sc1 writes)
+template <int KT>
+GNOT_DEV void round_rows_bf16(float (&a)[KT][4]) {
+#pragma unroll
+  for (int T = 0; T < KT; ++T)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) a[T][r] = bf16_lo(pk_bf16(a[T][r], 0.f));
+}
+
 // The fused soft-MoE combine (model.py:128-131 / 134-137): called by every workgroup of the expert grid
 // after its write-through stage stores.  Hand-off (MI355X_MICROARCH.md, "Valid forms", first table row):
 // every wave waits for its own stores (vmcnt(0)), a barrier, then ONE lane adds to the block's counter
@@ -97,6 +133,9 @@ GNOT_DEV void store_rows_sc1(const float (&v)[OT][4], rsrc_t r, int voff) {
 // counter for the next launch and, after a barrier, sums the block's E stage rows with sc1 loads, in
 // expert order, onto `base` (or 0): bitwise the separate combine pass it replaces.  One workgroup per CU
 // (the chain kernels' LDS), as that hand-off form requires.
+// B16 (bf16 mode, bf16 storage): the stage rows are RNE bf16 pair-interleaved rows (512 B per point), summed
+// in fp32 in the same order (the walk form rounds each expert's term the same way)
+template <bool B16>
 GNOT_DEV void moe_combine_last(const float* stage, long stage_stride, int E, const float* base, float* out,
                                int* counters, int blk, long row0, int nrows) {
   __shared__ int last;
@@ -109,6 +148,57 @@ GNOT_DEV void moe_combine_last(const float* stage, long stage_stride, int E, con
   }
   __syncthreads();
   if (!last) return;
+  if constexpr (B16) {
+    // 128 rows x 32 chunks of 16 B: thread t owns chunk c = t & 31 of rows (t >> 5) + 16 k, four rows per
+    // round.  Chunk c = 4 tp + g holds features 32 tp + 4 g .. +3 (half 0) and 32 tp + 16 + 4 g .. +3 (half 1)
+    constexpr int R = 4;
+    const long fo = row0 * 256;                   // fp32 rows of out / base
+    const long so = row0 * (kB16Row / 4);         // bf16 stage rows, in 4-byte units
+    const unsigned bytes = (unsigned)nrows * 1024u, sbytes = (unsigned)nrows * (unsigned)kB16Row;
+    const rsrc_t ro = make_rsrc(out + fo, bytes);
+    const rsrc_t rb = make_rsrc(base ? base + fo : out + fo, base ? bytes : 0u);
+    const int t = threadIdx.x, ch = t & 31, r0 = t >> 5;
+    const int f0 = 32 * (ch >> 2) + 4 * (ch & 3);   // first feature of half 0 (half 1: + 16)
+    for (int k = 0; k < 8; k += R) {
+      int vo[R], vs[R];
+      float4 lo[R], hi[R];
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const int row = r0 + 16 * (k + i);
+        vo[i] = row * 1024 + f0 * 4;
+        vs[i] = row * kB16Row + ch * 16;
+        lo[i] = base ? buf_load_f32x4(rb, vo[i], 0) : make_float4(0.f, 0.f, 0.f, 0.f);
+        hi[i] = base ? buf_load_f32x4(rb, vo[i] + 64, 0) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      for (int e0 = 0; e0 < E; e0 += 8) {
+        u32x4 s[8][R];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (e0 + j < E) {
+            const rsrc_t rs = make_rsrc(stage + (e0 + j) * stage_stride + so, sbytes);
+#pragma unroll
+            for (int i = 0; i < R; ++i) s[j][i] = __builtin_amdgcn_raw_buffer_load_b128(rs, vs[i], 0, kCpolSc1);
+          }
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (e0 + j < E) {
+#pragma unroll
+            for (int i = 0; i < R; ++i) {
+              lo[i].x += bf16_lo(s[j][i][0]); lo[i].y += bf16_hi(s[j][i][0]);
+              lo[i].z += bf16_lo(s[j][i][1]); lo[i].w += bf16_hi(s[j][i][1]);
+              hi[i].x += bf16_lo(s[j][i][2]); hi[i].y += bf16_hi(s[j][i][2]);
+              hi[i].z += bf16_lo(s[j][i][3]); hi[i].w += bf16_hi(s[j][i][3]);
+            }
+          }
+      }
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        buf_store_f32x4(lo[i], ro, vo[i]);
+        buf_store_f32x4(hi[i], ro, vo[i] + 64);
+      }
+    }
+    return;
+  }
   // 128 rows x 64 float4: thread t owns column group t & 63 of rows (t >> 6) + 8 k, four rows per round
   // with every expert's loads in flight (up to 36 16-byte loads per lane: the stage rows come from the
   // memory side, so the latency, not the bytes, sets the time); rows past the block's nrows read 0,
@@ -294,7 +384,7 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) 
   extern __shared__ __attribute__((aligned(16))) u32x4 c2lds[];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4;
   int blk, eg;
-  c2_grid_pos(a.nchains, !WALK && a.nchains > 1, blk, eg);
+  c2_grid_pos(a.nchains, WALK ? 0 : a.grid_mode, blk, eg);
   if ((long)blk * kC2Waves * 16 >= a.P) return;       // past the last block (whole workgroup, before any barrier)
   const long p = ((long)blk * kC2Waves + wave) * 16 + (lane & 15);
   const bool valid = p < a.P;
@@ -399,7 +489,9 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) 
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           // the product rounded on its own (no FMA contraction): the expert grid's s_e * y_e store + add
+          // (B16: the grid's bf16 stage value)
           float t = s * y[T][r];
+          if constexpr (B16) t = bf16_lo(pk_bf16(t, 0.f));
           asm volatile("" : "+v"(t));
           y[T][r] = acc[T][r] + t;
         }
@@ -441,7 +533,8 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) 
   }
   if constexpr (OTL == 16) {
     if (a.combine != nullptr) {               // fused combine: write-through stage rows (D = 256)
-      store_rows_sc1<OTL>(y, make_rsrc(a.Y + e * a.y_chain_stride + row0 * D, lay_bytes), voff);
+      if constexpr (B16) store_rows_b16_sc1<OTL>(y, make_rsrc(a.Y + e * a.y_chain_stride + rbase, lay_b16), rowb, lane);
+      else store_rows_sc1<OTL>(y, make_rsrc(a.Y + e * a.y_chain_stride + row0 * D, lay_bytes), voff);
       return;
     }
   }
@@ -453,7 +546,7 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) 
   } else {
     expert(eg);
     if (a.combine != nullptr)
-      moe_combine_last(a.Y, a.y_chain_stride, a.nchains, a.base, a.combine, a.counters, blk, row0, nrows);
+      moe_combine_last<B16>(a.Y, a.y_chain_stride, a.nchains, a.base, a.combine, a.counters, blk, row0, nrows);
   }
 }
 
@@ -593,7 +686,7 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) 
   extern __shared__ __attribute__((aligned(16))) u32x4 c2lds[];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), g = lane >> 4;
   int blk, eg;
-  c2_grid_pos(a.nchains, !WALK && a.nchains > 1, blk, eg);
+  c2_grid_pos(a.nchains, WALK ? 0 : a.grid_mode, blk, eg);
   if ((long)blk * kC2Waves * 16 >= a.P) return;       // past the last block (whole workgroup, before any barrier)
   const long p = ((long)blk * kC2Waves + wave) * 16 + (lane & 15);
   const bool valid = p < a.P;
@@ -735,6 +828,7 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) 
       for (int r = 0; r < 4; ++r) dx[o][r] = acc[r];
     }
     if constexpr (WALK) {
+      if constexpr (B16) round_rows_bf16<KT0>(dx);   // each expert's term as the grid's bf16 stage holds it
       if (e > e_begin) {
         float part[KT0][4];
         load_rows<KT0>(part, a.dX, a.lddx, p, valid, a.in_dim, lane);
@@ -745,7 +839,8 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) 
       }
       store_rows<KT0>(dx, a.dX, a.lddx, p, valid, a.in_dim, lane);
     } else if (KT0 == 16 && a.combine != nullptr) {   // fused combine: write-through stage rows (D = 256)
-      store_rows_sc1<KT0>(dx, make_rsrc(a.dX + e * a.dx_chain_stride + row0 * D, lay_bytes), voff);
+      if constexpr (B16) store_rows_b16_sc1<KT0>(dx, make_rsrc(a.dX + e * a.dx_chain_stride + rbase, lay_b16), rowb, lane);
+      else store_rows_sc1<KT0>(dx, make_rsrc(a.dX + e * a.dx_chain_stride + row0 * D, lay_bytes), voff);
     } else {
       store_rows<KT0>(dx, a.dX + e * a.dx_chain_stride, a.lddx, p, valid, a.in_dim, lane);
     }
@@ -756,7 +851,7 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) 
   } else {
     expert(eg);
     if (a.combine != nullptr)
-      moe_combine_last(a.dX, a.dx_chain_stride, a.nchains, nullptr, a.combine, a.counters, blk, row0, nrows);
+      moe_combine_last<B16>(a.dX, a.dx_chain_stride, a.nchains, nullptr, a.combine, a.counters, blk, row0, nrows);
   }
 }
 
@@ -764,9 +859,10 @@ template <int D, int NP>
 static hipError_t launch_chain2_d(const ChainArgs& a, bool bwd, hipStream_t s) {
   constexpr int DT = D / 16;
   const int nblocks = (a.P + 16 * kC2Waves - 1) / (16 * kC2Waves);
-  static const bool nogroup = std::getenv("GNOT_C2_NOGROUP") != nullptr;   // TEMP A/B
-  const bool grouped = !a.walk && a.nchains > 1 && !nogroup;
-  const dim3 grid = grouped ? dim3(c2_grid_size(nblocks, a.nchains, true)) : dim3(nblocks, a.walk ? 1 : a.nchains);
+  const int mode = a.walk ? 0 : c2_grid_mode(a.nchains);
+  const dim3 grid = mode ? dim3(c2_grid_size(nblocks, a.nchains, mode)) : dim3(nblocks, a.walk ? 1 : a.nchains);
+  ChainArgs b = a;
+  b.grid_mode = mode;
   const dim3 block(64 * kC2Waves);
   if (a.combine != nullptr && (a.walk || a.mode != CH_MOE || a.KT0 != DT || a.OTL != DT || !a.counters ||
                                (bwd ? (!a.dX || a.lddx != D || a.dx_chain_stride % 4) : (!a.Y || a.ldy != D || a.y_chain_stride % 4))))
@@ -788,10 +884,10 @@ static hipError_t launch_chain2_d(const ChainArgs& a, bool bwd, hipStream_t s) {
 #define GNOT_C2_B16(W_)                                                                                  \
   if (bwd) {                                                                                             \
     GNOT_C2_ATTR((chain2_bwd_kernel<D, DT, DT, 1, W_, true>));                                           \
-    hipLaunchKernelGGL((chain2_bwd_kernel<D, DT, DT, 1, W_, true>), grid, block, lds, s, a);             \
+    hipLaunchKernelGGL((chain2_bwd_kernel<D, DT, DT, 1, W_, true>), grid, block, lds, s, b);             \
   } else {                                                                                               \
     GNOT_C2_ATTR((chain2_fwd_kernel<D, DT, DT, true, 1, W_, true>));                                     \
-    hipLaunchKernelGGL((chain2_fwd_kernel<D, DT, DT, true, 1, W_, true>), grid, block, lds, s, a);       \
+    hipLaunchKernelGGL((chain2_fwd_kernel<D, DT, DT, true, 1, W_, true>), grid, block, lds, s, b);       \
   }
       if (a.walk) {
         GNOT_C2_B16(true)
@@ -808,13 +904,13 @@ static hipError_t launch_chain2_d(const ChainArgs& a, bool bwd, hipStream_t s) {
     if (a.mode != CH_MOE || a.KT0 != DT || a.OTL != DT) return hipErrorInvalidValue;
     if (bwd) {
       GNOT_C2_ATTR((chain2_bwd_kernel<D, DT, DT, NP, true>));
-      hipLaunchKernelGGL((chain2_bwd_kernel<D, DT, DT, NP, true>), grid, block, lds, s, a);
+      hipLaunchKernelGGL((chain2_bwd_kernel<D, DT, DT, NP, true>), grid, block, lds, s, b);
     } else if (a.save) {
       GNOT_C2_ATTR((chain2_fwd_kernel<D, DT, DT, true, NP, true>));
-      hipLaunchKernelGGL((chain2_fwd_kernel<D, DT, DT, true, NP, true>), grid, block, lds, s, a);
+      hipLaunchKernelGGL((chain2_fwd_kernel<D, DT, DT, true, NP, true>), grid, block, lds, s, b);
     } else {
       GNOT_C2_ATTR((chain2_fwd_kernel<D, DT, DT, false, NP, true>));
-      hipLaunchKernelGGL((chain2_fwd_kernel<D, DT, DT, false, NP, true>), grid, block, lds, s, a);
+      hipLaunchKernelGGL((chain2_fwd_kernel<D, DT, DT, false, NP, true>), grid, block, lds, s, b);
     }
     return hipGetLastError();
   }
@@ -822,13 +918,13 @@ static hipError_t launch_chain2_d(const ChainArgs& a, bool bwd, hipStream_t s) {
   if (a.KT0 == K0 && a.OTL == OL) {                                                                      \
     if (bwd) {                                                                                           \
       GNOT_C2_ATTR((chain2_bwd_kernel<D, K0, OL, NP, false>));                                           \
-      hipLaunchKernelGGL((chain2_bwd_kernel<D, K0, OL, NP, false>), grid, block, lds, s, a);             \
+      hipLaunchKernelGGL((chain2_bwd_kernel<D, K0, OL, NP, false>), grid, block, lds, s, b);             \
     } else if (a.save) {                                                                                 \
       GNOT_C2_ATTR((chain2_fwd_kernel<D, K0, OL, true, NP, false>));                                     \
-      hipLaunchKernelGGL((chain2_fwd_kernel<D, K0, OL, true, NP, false>), grid, block, lds, s, a);       \
+      hipLaunchKernelGGL((chain2_fwd_kernel<D, K0, OL, true, NP, false>), grid, block, lds, s, b);       \
     } else {                                                                                             \
       GNOT_C2_ATTR((chain2_fwd_kernel<D, K0, OL, false, NP, false>));                                    \
-      hipLaunchKernelGGL((chain2_fwd_kernel<D, K0, OL, false, NP, false>), grid, block, lds, s, a);      \
+      hipLaunchKernelGGL((chain2_fwd_kernel<D, K0, OL, false, NP, false>), grid, block, lds, s, b);      \
     }                                                                                                    \
     return hipGetLastError();                                                                            \
   }

@@ -176,6 +176,7 @@ struct gnot_plan {
   bool packed = false;
   bool fwd_done = false;
   bool bwd_done = false;      // a gnot_backward ran after the last gnot_forward (gnot_input_grads needs it)
+  bool ig_reduced = false;    // sharded: the input-function gradients of that backward are rank sums already
 
   // point sharding (gnot_plan_set_shard): sample b's points are split over `world` ranks
   int world = 1, rank = 0;
@@ -1063,8 +1064,6 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
     if (p->Q[i] >= (1L << 31) / 4) return fail(GNOT_E_INVALID, "input functions too large for 32-bit segment indices");
   p->training = training != 0;
   p->sharded = p->world > 1;
-  if (p->input_grads && p->sharded)
-    return fail(GNOT_E_INVALID, "input gradients are not available with point sharding (gnot_plan_set_input_grads)");
   if (p->sharded) {
     if ((int)p->nglob.size() != B) return fail(GNOT_E_INVALID, "gnot_plan_set_shard was declared for another B");
     for (int b = 0; b < B; ++b) {
@@ -1178,6 +1177,7 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
       C.add("dfn" + std::to_string(i), p->Q[i] * D, D);
     }
     if (p->input_grads) {
+      C.add("dtheta_ws", (long)p->B * std::max(p->th, 1), std::max(p->th, 1));   // d theta before the copy out
       C.add("dxin", P * r4(p->in + p->th), r4(p->in + p->th));
       C.add("dxg", P * r4(p->in), r4(p->in));
       for (int i = 0; i < I; ++i) C.add("dfnin" + std::to_string(i), p->Q[i] * r4(p->F), r4(p->F));
@@ -2020,6 +2020,7 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
   }
   p->readers.clear();
   p->bwd_done = true;
+  p->ig_reduced = false;
   return GNOT_OK;
 }
 
@@ -2035,11 +2036,26 @@ extern "C" int gnot_input_grads(gnot_plan* p, float* dx, float* dtheta, float* c
   const Buf& xin = p->bufs.at("dxin");
   const Buf& xg = p->bufs.at("dxg");
   if (dx) GNOT_CK(launch_add_cols(xin.p, xin.ld, xg.p, xg.ld, p->in, dx, p->P, s));
-  if (dtheta) GNOT_CK(launch_seg_colsum(xin.p, xin.ld, p->in, p->th, p->d_xoff, p->B, dtheta, s));
-  for (int i = 0; dfns && i < p->I; ++i) {
-    const Buf& f = p->bufs.at("dfnin" + std::to_string(i));
-    if (dfns[i]) GNOT_CK(launch_add_cols(f.p, f.ld, nullptr, 0, p->F, dfns[i], p->Q[i], s));
+  // point-sharded: x's rows are local, but theta (broadcast over ALL points of a sample) and the input
+  // functions (replicated on every rank, reached through every rank's attention states) get one partial
+  // gradient per rank -- summed over the ranks (every rank must call this: the sums are collectives)
+  float* dth = p->P_("dtheta_ws");
+  if (dtheta || p->sharded) GNOT_CK(launch_seg_colsum(xin.p, xin.ld, p->in, p->th, p->d_xoff, p->B, dth, s));
+  if (p->sharded && p->th > 0) {
+    Ctx c{p, s};
+    GNOT_RUN(shard_allreduce(c, dth, (long)p->B * p->th));
   }
+  if (dtheta && p->th > 0)
+    GNOT_CK(hipMemcpyAsync(dtheta, dth, (size_t)p->B * p->th * 4, hipMemcpyDeviceToDevice, s));
+  for (int i = 0; i < p->I; ++i) {
+    const Buf& f = p->bufs.at("dfnin" + std::to_string(i));
+    if (p->sharded && !p->ig_reduced) {
+      Ctx c{p, s};
+      GNOT_RUN(shard_allreduce(c, f.p, p->Q[i] * f.ld));
+    }
+    if (dfns && dfns[i]) GNOT_CK(launch_add_cols(f.p, f.ld, nullptr, 0, p->F, dfns[i], p->Q[i], s));
+  }
+  p->ig_reduced = true;
   return GNOT_OK;
 }
 

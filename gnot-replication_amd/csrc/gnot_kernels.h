@@ -102,6 +102,7 @@ struct ChainArgs {
   // int per 128-point block, zero between launches (each launch's last workgroups reset theirs)
   float* combine = nullptr;
   int* counters = nullptr;
+  int grid_mode = 0;                 // set by the launcher (chain2.hip c2_grid_pos)
   // CH_MOE, d = 256, np = 1 (bf16 mode): bf16 activation storage.  Saves and dZ are bf16 "pair-
   // interleaved" rows (gnot_common.h, 512 B per point; strides above then count 4-byte units, so a
   // [P, 256] bf16 layer is P * 128 of them).  Per chain, save slots 0 .. nlin-2 hold gelu'(h_l) of the

@@ -102,9 +102,11 @@ int gnot_plan_set_precision(gnot_plan* plan, int bf16);
  * torch.cat with the broadcast theta, the query encoder; the input functions feed their encoder
  * MLPs).  With on != 0 the backward also runs the first Linear's backward-data of those four encoders;
  * gnot_input_grads then writes dx [P, input_dim], dtheta [B, theta_dim] (sums over each sample's
- * points) and dfns[i] [Q_i, input_func_dim] (any pointer may be null: skipped).  Training plans only;
- * not with point sharding (theta's gradient would be a per-rank partial sum).  Changing it invalidates
- * the batch (set_batch + bind again). */
+ * points) and dfns[i] [Q_i, input_func_dim] (any pointer may be null: skipped).  Training plans only.
+ * With point sharding dx holds this rank's rows, and dtheta / dfns -- one partial per rank, theta being
+ * broadcast over all points and the input functions replicated -- are summed over the ranks through the
+ * plan's gnot_comm (every rank must call gnot_input_grads).  Changing it invalidates the batch
+ * (set_batch + bind again). */
 int gnot_plan_set_input_grads(gnot_plan* plan, int on);
 int gnot_input_grads(gnot_plan* plan, float* dx, float* dtheta, float* const* dfns, void* stream);
 

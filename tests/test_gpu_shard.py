@@ -169,3 +169,88 @@ def test_point_sharded_configs3_widths_70k_points(mid_case):
         p.join(timeout=60)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert not errs, errs
+
+
+def _rank_input_grads(rank, world, port, cfg, Ns, Ms, q):
+    """Input gradients of a point-sharded batch: each rank differentiates its slice of x; theta and the
+    (replicated) input functions get one partial per rank, summed over the ranks inside gnot_input_grads."""
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "gnot-replication_amd"), os.path.join(ROOT, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from golden_util import model_args
+        from gnot_amd import GNOT
+        from gnot_amd import parallel as par
+        from test_gpu_input_grads import _port_grads, _rel
+        torch.manual_seed(5)
+        m = GNOT(*model_args(cfg))
+        sd64 = {k: v.detach().double() for k, v in m.state_dict().items()}
+        dev = torch.device("cuda", 0)
+        m = m.to(dev)
+        m.set_point_shard(par.PointShardComm(stage_via_host=True))
+        rng = np.random.default_rng(3)
+        I = cfg["n_input_functions"]
+        xs = [rng.random((n, cfg["input_dim"])) for n in Ns]
+        thetas = [rng.random(cfg["theta_dim"]) for _ in Ns]
+        fns_ps = [[rng.random((Ms[i][b], cfg["input_func_dim"])) for i in range(I)] for b in range(len(Ns))]
+        Gs = [rng.standard_normal((n, cfg["out_dim"])) for n in Ns]
+        loc_off, ranges = par.shard_offsets(Ns, rank, world)
+        t = lambda a: torch.tensor(np.ascontiguousarray(a), dtype=torch.float32, device=dev)
+        x = t(np.concatenate([xs[b][lo:hi] for b, (lo, hi) in enumerate(ranges)])).requires_grad_(True)
+        th = t(np.stack(thetas)).requires_grad_(True)
+        fns = [t(np.concatenate([fns_ps[b][i] for b in range(len(Ns))])).requires_grad_(True) for i in range(I)]
+        fn_offs = [np.concatenate([[0], np.cumsum([Ms[i][b] for b in range(len(Ns))])]).tolist() for i in range(I)]
+        G = t(np.concatenate([Gs[b][lo:hi] for b, (lo, hi) in enumerate(ranges)]))
+        out = m.forward_packed(x, loc_off, th, fns, fn_offs, n_global=Ns)
+        (out * G).sum().backward()
+        torch.cuda.synchronize()
+        got = (x.grad.double().cpu().numpy(), th.grad.double().cpu().numpy(), [f.grad.double().cpu().numpy() for f in fns])
+        parts = [None] * world
+        dist.all_gather_object(parts, (ranges, got))
+        if rank == 0:
+            rx, rt, rf = _port_grads(cfg, sd64, xs, thetas, fns_ps, Gs)
+            dx = [np.zeros_like(r) for r in rx]
+            for rgs, (gx, _, _) in parts:
+                k = 0
+                for b, (lo, hi) in enumerate(rgs):
+                    dx[b][lo:hi] = gx[k:k + hi - lo]
+                    k += hi - lo
+            errs = []
+            e = _rel(np.concatenate(dx), np.concatenate(rx))
+            if e > 1e-4:
+                errs.append(f"dx {e:.3e}")
+            for r, (_, gt, gf) in enumerate(parts):   # every rank holds the rank sums
+                e = _rel(gt, np.stack(rt))
+                if e > 1e-4:
+                    errs.append(f"rank {r} dtheta {e:.3e}")
+                for i in range(I):
+                    e = _rel(gf[i], np.concatenate([rf[b][i] for b in range(len(Ns))]))
+                    if e > 1e-4:
+                        errs.append(f"rank {r} dfn{i} {e:.3e}")
+            q.put(errs)
+    except Exception as e:
+        if rank == 0:
+            q.put([f"rank0 exception: {e!r}"])
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_point_sharded_input_grads():
+    """dx (this rank's rows), dtheta and the input-function gradients (rank sums) of a batch point-sharded
+    over 2 ranks vs float64 autograd of the stock-torch port (one reference call per sample) at 1e-4."""
+    cfg = dict(input_dim=2, theta_dim=2, input_func_dim=3, out_dim=1, n_attn_layers=2, d=64,
+               n_mlp_num_layers=3, n_expert=3, n_head=4, n_input_functions=1)
+    Ns, Ms = [300, 173], [[120, 77]]
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_input_grads, args=(r, world, port, cfg, Ns, Ms, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    errs = q.get(timeout=200)
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert not errs, errs
