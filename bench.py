@@ -520,11 +520,10 @@ def main():
         torch.cuda.synchronize()
         rkind = args.roofline_kernel
         if rkind == "auto":
-            # bf16 mode: the soft-MoE weight gradients are their own class (wgrad_b16); what stays in
-            # "wgrad" are the attention / encoder projections' weight gradients (~1.2 of the step's ~34
-            # TFLOP), whose side-stream launches mostly wait for CUs the MoE chains hold (their in-step
-            # durations are not their cost), so they do not compete for the roofline line
-            pick = [k for k in kinds if not ("wgrad_b16" in kinds and k == "wgrad")]
+            # the class with the most device time; the weight gradients run on the caller's stream after
+            # their chain backward (engine.cpp serial_wgrad), so every class time is its own serial cost.
+            # bf16 mode: the soft-MoE weight gradients are their own class (wgrad_b16)
+            pick = list(kinds)
             rkind = max(pick, key=lambda k: kinds[k][0])
 
         step = eager_step

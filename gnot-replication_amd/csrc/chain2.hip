@@ -63,11 +63,13 @@ struct C2Lds {
 // share one, MI355X_MICROARCH.md "Workgroup dispatch"); speed only, nothing depends on placement.
 //   mode 1 "grouped": w = 8 (E (b / 8) + e) + b % 8 -- the E experts of a block run at the same time on
 //          ONE XCD and read the block's input rows (forward: the MoE input; backward: dquery, the scores)
-//          once from HBM into its L2; every XCD streams all E experts' weights;
-//   mode 2 "expert per XCD" (E divides 8): XCD x runs expert x % E only, so its L2 holds one expert's
-//          weight images, and the blocks advance at the same pace on every XCD, so the E reads of a
-//          block's input rows fall together in the shared Infinity Cache;
-//   mode 0: blockIdx.x = block, blockIdx.y = expert (the walk form and single chains always).
+//          once from HBM into its L2, and the fused combine's last workgroup reads the stage rows its
+//          siblings wrote through that same L2; every XCD streams all E experts' weights;
+//   mode 0: blockIdx.x = block, blockIdx.y = expert (the walk form and single chains).
+// Measured at configs[2] (262,144 points, E = 8, d = 256; profiles/r04_chain_grid.txt): mode 1 against
+// mode 0, bf16x6 forward 6.76 / 6.81 ms, backward 8.27 / 9.02; bf16 storage 4.01 / 4.31 and 3.84 / 4.12.
+// An "expert per XCD" deal (XCD x runs expert x % E) was slower still with the fused combine (forward
+// + combine 10.2 ms) and is gone.
 GNOT_DEV void c2_grid_pos(int E, int mode, int& blk, int& e) {
   if (mode == 0 || gridDim.y > 1) {
     blk = (int)blockIdx.x;
@@ -75,26 +77,13 @@ GNOT_DEV void c2_grid_pos(int E, int mode, int& blk, int& e) {
     return;
   }
   const int w = (int)blockIdx.x, x = w & 7, s = w >> 3;
-  if (mode == 2) {
-    e = x % E;
-    blk = s * (8 / E) + x / E;
-    return;
-  }
   e = s % E;
   blk = (s / E) * 8 + x;
 }
-// the grid mode of an expert grid of E chains (env GNOT_C2_GRID: A/B runs)
-static int c2_grid_mode(int E) {
-  static const int env = std::getenv("GNOT_C2_GRID") ? std::atoi(std::getenv("GNOT_C2_GRID")) : -1;
-  if (E <= 1) return 0;
-  if (env >= 0) return (env == 2 && 8 % E != 0) ? 1 : env;
-  return 8 % E == 0 ? 2 : 1;
-}
-// 1-D grid of the grid modes 1 / 2 (the ids past the last block exit at once)
-inline unsigned c2_grid_size(int nblocks, int E, int mode) {
-  if (mode == 2) return (unsigned)((nblocks + 8 / E - 1) / (8 / E)) * 8u;
-  return (unsigned)((nblocks + 7) / 8 * 8) * (unsigned)E;
-}
+// the grid mode of an expert grid of E chains
+static int c2_grid_mode(int E) { return E <= 1 ? 0 : 1; }
+// 1-D grid of mode 1 (the ids past the last block exit at once)
+inline unsigned c2_grid_size(int nblocks, int E) { return (unsigned)((nblocks + 7) / 8 * 8) * (unsigned)E; }
 
 // OT point-form tiles of this lane's row (rows of 256 fp32, voff = row-in-block * 1 KiB + 16 B * g) stored
 // write-through (sc1: the bytes reach the device-coherent level, so another XCD's sc1 loads see them)
@@ -403,9 +392,6 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) 
   // float offset of the workgroup's first row in a layer (fp32: D floats per row; B16: 512 B = 128 floats)
   const long rbase = row0 * (B16 ? kB16Row / 4 : D);
   C2Pipe pp{c2lds, LD::WB, 0, wave, lane};
-#ifdef GNOT_EXP_PRIO
-  if (wave >= 4) __builtin_amdgcn_s_setprio(1);     // EXPERIMENT: static priority for the second half
-#endif
   constexpr int CH = c2f_pair<NP>() ? 2 : 1;         // output tiles per weight chunk
   // a layer's first wait: the saves the previous layer issued after its last weight DMA (its last
   // tile's stream + the final epilogue; pair mode: its last pair's two tiles + the final epilogue)
@@ -444,7 +430,7 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) 
     u32x4 b0[KB0][NP];
     c2_split<KT0, NP>(x0, b0);
     int pend0 = 0;
-    if constexpr (B16) {
+    if constexpr (B16 && SAVE) {
       // the shared MoE input (Linear 0's operand): chain 0 only
       if (e == 0) {
         if constexpr (KB0 == KB) pend0 = store_in(a.save + nl * a.save_layer_stride, b0, KB0);
@@ -458,7 +444,7 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) 
   }
   for (int l = 1; l < nl - 1; ++l) {
     c2_split<DT, NP>(nx, bp);
-    const int pin = B16 ? store_in(save + (nl + l) * a.save_layer_stride, bp, KB) : 0;
+    const int pin = B16 && SAVE ? store_in(save + (nl + l) * a.save_layer_stride, bp, KB) : 0;
     const int nb = l + 1 == nl - 1 ? 16 * OTL * 4 : 16 * DT * 4;
     c2f_layer<DT, KB, true, SAVE, NP, B16>(pp, wp(l), bp, bsel, rs(l), svoff, wp(l + 1),
                                            (l + 1 == nl - 1 ? (OTL < CH ? OTL : CH) : CH) * c2_tile_u4(KB, NP),
@@ -467,7 +453,7 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) 
   }
   float y[OTL][4];
   c2_split<DT, NP>(nx, bp);
-  const int pin_last = B16 ? store_in(save + (2 * nl - 1) * a.save_layer_stride, bp, KB) : 0;
+  const int pin_last = B16 && SAVE ? store_in(save + (2 * nl - 1) * a.save_layer_stride, bp, KB) : 0;
   c2f_layer<OTL, KB, false, SAVE, NP, B16>(pp, wp(nl - 1), bp, bsel, rs(nl - 1), svoff, nullptr, 0, nullptr, 0,
                                            pend_next + pin_last, g, y);
   if constexpr (WALK) {
@@ -702,9 +688,6 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) 
   const long rbase = row0 * (B16 ? kB16Row / 4 : D);
   const int lvoff = B16 ? rowb : voff;               // what the layers address rows with
   C2Pipe pp{c2lds, LD::WB, 0, wave, lane};
-#ifdef GNOT_EXP_PRIO
-  if (wave >= 4) __builtin_amdgcn_s_setprio(1);     // EXPERIMENT: static priority for the second half
-#endif
   constexpr int e_begin = 0;
   auto expert = [&](int e) __attribute__((always_inline)) {
   const ChainLayer* L = a.layers + e * nl;
@@ -860,7 +843,7 @@ static hipError_t launch_chain2_d(const ChainArgs& a, bool bwd, hipStream_t s) {
   constexpr int DT = D / 16;
   const int nblocks = (a.P + 16 * kC2Waves - 1) / (16 * kC2Waves);
   const int mode = a.walk ? 0 : c2_grid_mode(a.nchains);
-  const dim3 grid = mode ? dim3(c2_grid_size(nblocks, a.nchains, mode)) : dim3(nblocks, a.walk ? 1 : a.nchains);
+  const dim3 grid = mode ? dim3(c2_grid_size(nblocks, a.nchains)) : dim3(nblocks, a.walk ? 1 : a.nchains);
   ChainArgs b = a;
   b.grid_mode = mode;
   const dim3 block(64 * kC2Waves);
@@ -878,16 +861,22 @@ static hipError_t launch_chain2_d(const ChainArgs& a, bool bwd, hipStream_t s) {
     }                                                                                                    \
   } while (0)
   if (a.b16s) {
-    // bf16 storage: soft-MoE experts (d x d chains) in bf16 mode, training (saves) only
+    // bf16 storage: soft-MoE experts (d x d chains) in bf16 mode.  The expert terms are bf16 (the stage
+    // rows, or the walk form's rounding), so the expert grid sums them with the fused combine only;
+    // a forward without saves (inference, MoE recompute's first pass) rounds its terms alike
     if constexpr (NP == 1) {
-      if (a.mode != CH_MOE || a.KT0 != DT || a.OTL != DT || (!bwd && !a.save)) return hipErrorInvalidValue;
+      if (a.mode != CH_MOE || a.KT0 != DT || a.OTL != DT) return hipErrorInvalidValue;
+      if (!a.walk && !a.combine && (bwd || a.Y)) return hipErrorInvalidValue;
 #define GNOT_C2_B16(W_)                                                                                  \
   if (bwd) {                                                                                             \
     GNOT_C2_ATTR((chain2_bwd_kernel<D, DT, DT, 1, W_, true>));                                           \
     hipLaunchKernelGGL((chain2_bwd_kernel<D, DT, DT, 1, W_, true>), grid, block, lds, s, b);             \
-  } else {                                                                                               \
+  } else if (a.save) {                                                                                   \
     GNOT_C2_ATTR((chain2_fwd_kernel<D, DT, DT, true, 1, W_, true>));                                     \
     hipLaunchKernelGGL((chain2_fwd_kernel<D, DT, DT, true, 1, W_, true>), grid, block, lds, s, b);       \
+  } else {                                                                                               \
+    GNOT_C2_ATTR((chain2_fwd_kernel<D, DT, DT, false, 1, W_, true>));                                    \
+    hipLaunchKernelGGL((chain2_fwd_kernel<D, DT, DT, false, 1, W_, true>), grid, block, lds, s, b);      \
   }
       if (a.walk) {
         GNOT_C2_B16(true)

@@ -146,13 +146,15 @@ struct gnot_plan {
   size_t table_bytes = 0;
   size_t slab_wgrad_floats = 0, slab_state_floats = 0;
 
-  // backward overlap: weight-gradient GEMMs run on a side stream; every buffer they read is
-  // double-buffered and guarded by the event of its last side-stream reader
+  // weight-gradient groups run on the caller's stream after the chain backward that produced their dZ.
+  // env GNOT_WGRAD_OVERLAP = 1 (read when the plan is created) forks them onto the side stream instead;
+  // every buffer they read is then double-buffered and guarded by the event of its last side-stream
+  // reader.  Measured at configs[2] on one box, interleaved (profiles/r04_wgrad_overlap_ab.txt): 235.3 /
+  // 236.2 ms per step serial against 236.8 / 236.7 overlapped -- the concurrent chain kernels and GEMMs
+  // share the same CUs, so the overlap buys nothing, and the serial order keeps the kernel classes apart
   hipStream_t side = nullptr;
   hipStream_t side2 = nullptr;          // input-function branch, concurrent with the query branch
-  // weight gradients on the caller's stream (no side-stream overlap): env GNOT_SERIAL_WGRAD, read when
-  // the plan is created (so a test can build both forms in one process)
-  bool serial_wgrad = false;
+  bool serial_wgrad = true;
   std::vector<hipEvent_t> evs;
   size_t ev_next = 0;
   // pinned staging ring for the table uploads of gnot_plan_bind_workspace_async: slot k is rewritten
@@ -326,7 +328,7 @@ extern "C" int gnot_plan_create(const gnot_config* cfg, gnot_plan** out) {
   }
   p->W.assign(p->n_lin(), nullptr);
   p->b.assign(p->n_lin(), nullptr);
-  if (const char* sw = std::getenv("GNOT_SERIAL_WGRAD")) p->serial_wgrad = sw[0] == '1';
+  if (const char* ov = std::getenv("GNOT_WGRAD_OVERLAP")) p->serial_wgrad = ov[0] != '1';
   *out = p;
   return GNOT_OK;
 }
@@ -1560,8 +1562,8 @@ int grad_allreduce(gnot_plan* p, const WgradGroup& G, hipEvent_t done) {
   return GNOT_OK;
 }
 
-// weight gradients: forked onto the side stream (off the critical path); `reads` are the main-stream
-// buffers the group consumes, guarded until it finishes
+// weight gradients: on the caller's stream (default), or forked onto the side stream (GNOT_WGRAD_OVERLAP);
+// `reads` are the main-stream buffers the group consumes, guarded until it finishes
 int run_wgrad_side(Ctx& c, const WgradGroup& G, std::initializer_list<const float*> reads) {
   if (G.jobs.empty()) return GNOT_OK;
   gnot_plan* p = c.p;
@@ -1734,9 +1736,13 @@ int attn_backward(Ctx& c, int l, bool cross) {
 }  // namespace
 
 // the soft-MoE experts of one call: walk form (d = 256, chain2.hip) or the expert grid, whose last
-// workgroup per 128-point block sums the experts (the fused combine, d = 256) -- moe_combine at d < 256
+// workgroup per 128-point block sums the experts (the fused combine, d = 256) or a moe_combine pass over
+// the [E, P, d] stage.  The fused combine runs in every backward at d = 256 and in the forward of the
+// bf16 mode (bf16 stage rows); the bf16x6 forward keeps the separate pass.  Measured at configs[2]
+// (262,144 points, E = 8; profiles/r04_chain_grid.txt): bf16x6 forward 6.76 ms + 0.47 pass against 7.51
+// fused, backward 8.27 + 0.47 against 8.73; bf16 storage forward 4.01 + 0.47 against 4.08 fused
 static bool moe_walk(gnot_plan* p) { return p->moe_walk; }
-static bool moe_fused(gnot_plan* p) { return p->D == 256 && !p->moe_walk; }
+static bool moe_fused(gnot_plan* p, bool bwd) { return p->D == 256 && !p->moe_walk && (bwd || p->b16s()); }
 // save (and dZ) layout of a soft-MoE chain call: fp32 [NL][P][D] per expert, or in bf16 mode 2 NL bf16
 // layers per expert (ChainArgs::b16s)
 static void moe_save_strides(gnot_plan* p, ChainArgs& a) {
@@ -1754,18 +1760,19 @@ static int moe_forward(Ctx& c, const ChainTable& T, const float* in, const float
   ChainArgs a = chain_args(p, T, P);
   a.X = in; a.ldx = D; a.ldy = D;
   a.scores = p->P_("scores"); a.ldsc = (int)p->bufs["scores"].ld; a.mode = CH_MOE;
-  if (save) { a.save = save; moe_save_strides(p, a); }
+  moe_save_strides(p, a);                 // bf16 mode: bf16 expert terms with or without saves
+  a.save = save;
   if (walk) {
     a.walk = 1; a.Y = qout; a.base = qin;
   } else {
     a.Y = p->P_("stage"); a.y_chain_stride = P * D;
-    if (moe_fused(p)) { a.base = qin; a.combine = qout; a.counters = reinterpret_cast<int*>(p->P_("moe_cnt")); }
+    if (moe_fused(p, false)) { a.base = qin; a.combine = qout; a.counters = reinterpret_cast<int*>(p->P_("moe_cnt")); }
   }
   {
     ProfScope ps(c, "moe_fwd", 2.0 * E * P * NL * (double)D * D);
     GNOT_CK(launch_chain_fwd(a, c.s));
   }
-  if (!walk && !moe_fused(p)) GNOT_CK(launch_moe_combine(qin, p->P_("stage"), P * D, E, qout, P * D, c.s));
+  if (!walk && !moe_fused(p, false)) GNOT_CK(launch_moe_combine(qin, p->P_("stage"), P * D, E, qout, P * D, c.s));
   return GNOT_OK;
 }
 
@@ -1945,10 +1952,10 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
         a.walk = 1; a.dX = dsum; a.lddx = D; a.dx_chain_stride = 0;
       } else {
         a.dX = stage; a.lddx = D; a.dx_chain_stride = P * D;
-        if (moe_fused(p)) { a.combine = dsum; a.counters = reinterpret_cast<int*>(p->P_("moe_cnt")); }
+        if (moe_fused(p, true)) { a.combine = dsum; a.counters = reinterpret_cast<int*>(p->P_("moe_cnt")); }
       }
       GNOT_RUN(chain_bwd(a, m1 ? p->k_m1(l) : p->k_m2(l), P, m1 ? p->wg_m1[l] : p->wg_m2[l], "moe_bwd"));
-      if (!walk && !moe_fused(p)) GNOT_CK(launch_moe_combine(nullptr, stage, P * D, E, dsum, P * D, c.s));
+      if (!walk && !moe_fused(p, true)) GNOT_CK(launch_moe_combine(nullptr, stage, P * D, E, dsum, P * D, c.s));
       // m2: self attention (model.py:133) ; m1: cross attention (model.py:127)
       GNOT_RUN(attn_backward(c, l, m1));
     }

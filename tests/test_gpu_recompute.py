@@ -42,10 +42,10 @@ def test_recompute_matches_saved_activations_bitwise(d, E, I, prec):
 
 
 @pytest.mark.parametrize("prec", ["fp32", "bf16"])
-def test_serial_weight_gradients_match_side_stream_bitwise(prec, monkeypatch):
-    """GNOT_SERIAL_WGRAD=1 (read when the plan is created): every weight-gradient group on the caller's
-    stream instead of the side stream -- the same kernels in the same order per group, so outputs and
-    gradients are bitwise those of the overlapped default (configs[2] widths, input functions)."""
+def test_side_stream_weight_gradients_match_serial_bitwise(prec, monkeypatch):
+    """GNOT_WGRAD_OVERLAP=1 (read when the plan is created): every weight-gradient group forked onto the
+    side stream instead of the caller's stream -- the same kernels in the same order per group, so outputs
+    and gradients are bitwise those of the serial default (configs[2] widths, input functions)."""
     from gnot_amd import GNOT
     dev = torch.device("cuda")
     g = torch.Generator(device="cpu").manual_seed(21)
@@ -55,8 +55,8 @@ def test_serial_weight_gradients_match_side_stream_bitwise(prec, monkeypatch):
     fns = [torch.rand(300, 3, generator=g).to(dev)]
     tgt = torch.randn(x_off[-1], 1, generator=g).to(dev)
     res = []
-    for serial in ("0", "1"):
-        monkeypatch.setenv("GNOT_SERIAL_WGRAD", serial)
+    for overlap in ("0", "1"):
+        monkeypatch.setenv("GNOT_WGRAD_OVERLAP", overlap)
         torch.manual_seed(7)
         model = GNOT(3, 1, 3, 1, 2, 256, 4, 256, 256, 8, 8, 1).to(dev)
         model.set_precision(prec)

@@ -219,7 +219,7 @@ def _rank_input_grads(rank, world, port, cfg, Ns, Ms, q):
             e = _rel(np.concatenate(dx), np.concatenate(rx))
             if e > 1e-4:
                 errs.append(f"dx {e:.3e}")
-            for r, (_, gt, gf) in enumerate(parts):   # every rank holds the rank sums
+            for r, (_, (_, gt, gf)) in enumerate(parts):   # every rank holds the rank sums
                 e = _rel(gt, np.stack(rt))
                 if e > 1e-4:
                     errs.append(f"rank {r} dtheta {e:.3e}")
