@@ -1,7 +1,9 @@
 """configs[2] at its FULL size (one 262,144-point 3-D mesh, d=256, 8 experts, 4 blocks, 805 input-function
 points) -- far past what the float64 oracle can run, so checked through size-independent properties:
-finite outputs and gradients, bitwise-repeatable steps (deterministic reductions), and a RelL2 loss that
-decreases over a few AdamW steps on a fixed target (main.py:50-103)."""
+finite outputs and gradients, bitwise-repeatable steps (deterministic reductions), an inference forward
+(no saves) bitwise equal to the training forward, and a RelL2 loss that decreases over a few AdamW steps
+on a fixed target (main.py:50-103).  Both arithmetics: fp32 (bf16x6) and the bf16 mode, each in its
+default soft-MoE form (the expert grid; fused combine in the backward, and in the bf16 forward)."""
 import pytest
 import torch
 
@@ -11,12 +13,14 @@ N, M = 262144, 805
 
 
 @pytest.mark.timeout(300)
-def test_configs2_full_size_properties():
+@pytest.mark.parametrize("prec", ["fp32", "bf16"])
+def test_configs2_full_size_properties(prec):
     from gnot_amd import GNOT
     from gnot_amd import train as gtrain
     dev = torch.device("cuda")
     torch.manual_seed(1234)
     model = GNOT(3, 1, 3, 1, 4, 256, 4, 256, 256, 8, 8, 1).to(dev)
+    model.set_precision(prec)
     g = torch.Generator(device="cpu").manual_seed(100)
     x = torch.rand(N, 3, generator=g).to(dev)
     theta = torch.rand(1, 1, generator=g).to(dev)
@@ -40,6 +44,11 @@ def test_configs2_full_size_properties():
     assert torch.equal(o1, o2) and l1 == l2
     assert all(torch.equal(a, b) for a, b in zip(g1, g2)), "repeated step differs bitwise"
     del o2, g2
+    with torch.no_grad():                        # inference plan: no saves, the same arithmetic
+        o3 = model.forward_packed(x, x_off, theta, fns, fn_offs)
+    torch.cuda.synchronize()
+    assert torch.equal(o1, o3), f"inference forward differs: {float((o1 - o3).abs().max()):.3e}"
+    del o3
 
     opt = torch.optim.AdamW(model.parameters(), lr=1e-3)
     losses = [l1]
