@@ -146,15 +146,20 @@ struct gnot_plan {
   size_t table_bytes = 0;
   size_t slab_wgrad_floats = 0, slab_state_floats = 0;
 
-  // weight-gradient groups run on the caller's stream after the chain backward that produced their dZ.
-  // env GNOT_WGRAD_OVERLAP = 1 (read when the plan is created) forks them onto the side stream instead;
-  // every buffer they read is then double-buffered and guarded by the event of its last side-stream
-  // reader.  Measured at configs[2] on one box, interleaved (profiles/r04_wgrad_overlap_ab.txt): 235.3 /
-  // 236.2 ms per step serial against 236.8 / 236.7 overlapped -- the concurrent chain kernels and GEMMs
-  // share the same CUs, so the overlap buys nothing, and the serial order keeps the kernel classes apart
+  // weight-gradient groups run on the caller's stream after the chain backward that produced their dZ,
+  // or forked onto the side stream; every buffer a forked group reads is double-buffered and guarded
+  // by the event of its last side-stream reader.  Measured, one box each, interleaved x2
+  // (profiles/r04_wgrad_overlap_ab.txt): configs[2] (262,144 points) 235.3 / 236.2 ms per step serial
+  // against 236.8 / 236.7 forked -- the chains and GEMMs fill every CU, so overlapping them buys
+  // nothing; configs[1] (10,000 points, d = 128) 4.12 / 4.12 serial against 3.64 / 3.72 forked and
+  // configs[0] (16,384 points) 9.62 / 9.65 against 9.56 / 9.55 -- small launches leave CUs idle that
+  // the concurrent GEMMs fill.  So plans below kWgradSerialPoints fork, larger ones run serially; env
+  // GNOT_WGRAD_OVERLAP = 0 / 1 (read when the plan is created) forces either form (bitwise equal).
+  static constexpr long kWgradSerialPoints = 65536;
   hipStream_t side = nullptr;
   hipStream_t side2 = nullptr;          // input-function branch, concurrent with the query branch
-  bool serial_wgrad = true;
+  int wgrad_overlap_env = -1;
+  bool serial_wgrad() const { return wgrad_overlap_env >= 0 ? wgrad_overlap_env == 0 : P >= kWgradSerialPoints; }
   std::vector<hipEvent_t> evs;
   size_t ev_next = 0;
   // pinned staging ring for the table uploads of gnot_plan_bind_workspace_async: slot k is rewritten
@@ -328,7 +333,7 @@ extern "C" int gnot_plan_create(const gnot_config* cfg, gnot_plan** out) {
   }
   p->W.assign(p->n_lin(), nullptr);
   p->b.assign(p->n_lin(), nullptr);
-  if (const char* ov = std::getenv("GNOT_WGRAD_OVERLAP")) p->serial_wgrad = ov[0] != '1';
+  if (const char* ov = std::getenv("GNOT_WGRAD_OVERLAP")) p->wgrad_overlap_env = ov[0] == '1' ? 1 : 0;
   *out = p;
   return GNOT_OK;
 }
@@ -1562,12 +1567,12 @@ int grad_allreduce(gnot_plan* p, const WgradGroup& G, hipEvent_t done) {
   return GNOT_OK;
 }
 
-// weight gradients: on the caller's stream (default), or forked onto the side stream (GNOT_WGRAD_OVERLAP);
+// weight gradients: on the caller's stream (plans of >= 65,536 points), or forked onto the side stream;
 // `reads` are the main-stream buffers the group consumes, guarded until it finishes
 int run_wgrad_side(Ctx& c, const WgradGroup& G, std::initializer_list<const float*> reads) {
   if (G.jobs.empty()) return GNOT_OK;
   gnot_plan* p = c.p;
-  const bool serial = p->serial_wgrad;
+  const bool serial = p->serial_wgrad();
   // Only the caller's (capture-origin) stream forks to the side stream.  A fork from the forked
   // input-function stream side2 segfaults the HIP runtime in hipStreamEndCapture (ROCm 7.2, torch
   // 2.10), while eager execution of the same sequence is correct.  Four topologies, each run once:
