@@ -85,6 +85,12 @@ using namespace gnot;
 struct gnot_plan {
   gnot_config c{};
   int D = 0, H = 0, dh = 0, E = 0, NL = 0, L = 0, I = 0, KI = 0, DT = 0;
+  // Dr: the model's hidden width (n_embed); D: the width the kernels run, Dr rounded up to whole
+  // 16-wide tiles when Dr is not one the kernels take (gnot_plan_create).  Every activation row keeps D
+  // columns whose pad columns Dr .. D-1 stay exact zeros (zero weight rows / columns and biases in the
+  // packed images, pad columns of the feature softmax zeroed); parameters and gradients have Dr.
+  int Dr = 0;
+  bool padded() const { return Dr != D; }
   int in = 0, th = 0, F = 0, out = 0;
   std::vector<int> lin_o, lin_i;   // out / in features per canonical Linear
   std::vector<const float*> W, b;
@@ -285,15 +291,18 @@ extern "C" int gnot_plan_create(const gnot_config* cfg, gnot_plan** out) {
     return fail(GNOT_E_INVALID,
                 "n_attn_hidden_dim, n_mlp_hidden_dim and n_input_hidden_dim must be equal (the residual "
                 "adds of model.py:131/137 need it)");
-  const int D = c.n_attn_hidden_dim;
-  if (c.n_head <= 0 || D % c.n_head != 0)
+  const int Dr = c.n_attn_hidden_dim;
+  if (c.n_head <= 0 || Dr <= 0 || Dr % c.n_head != 0)
     return fail(GNOT_E_INVALID, "n_embed should be divisible by head");   // model.py:41
-  const int dh = D / c.n_head;
+  const int dh = Dr / c.n_head;
   // chain.hip / linear.hip run any multiple of 16 up to 192 (whole 16-wide MFMA tiles, activations in
   // registers), chain2.hip / linear2.hip d = 256; the attention passes any head width that is a multiple
-  // of 4 up to 64 (4-aligned lane slices, attn.hip; the fp32-MFMA forms at 16 / 32 / 64)
+  // of 4 up to 64 (4-aligned lane slices, attn.hip; the fp32-MFMA forms at 16 / 32 / 64).  A width below
+  // 192 that is not a multiple of 16 runs padded to the next multiple (Dr real columns + zero pads)
+  int D = Dr;
+  if (Dr % 16 != 0 && Dr < 192) D = (Dr + 15) / 16 * 16;
   if (!((D % 16 == 0 && D >= 16 && D <= 192) || D == 256))
-    return fail(GNOT_E_INVALID, "hidden width must be a multiple of 16 up to 192, or 256, on the MI355X kernels");
+    return fail(GNOT_E_INVALID, "hidden width must be at most 192, or 256, on the MI355X kernels");
   if (dh % 4 != 0 || dh > 64)
     return fail(GNOT_E_INVALID, "head width d/n_head must be a multiple of 4 up to 64 on the MI355X kernels");
   // the projections' fused feature softmax needs whole heads per workgroup: linear2.hip (d = 256) takes
@@ -305,28 +314,29 @@ extern "C" int gnot_plan_create(const gnot_config* cfg, gnot_plan** out) {
     return fail(GNOT_E_INVALID, "no projection tiling keeps whole heads of this head width on the MI355X kernels");
   if (c.n_expert < 1 || c.n_attn_layers < 0 || c.n_input_functions < 0 || c.n_input_functions > 8)
     return fail(GNOT_E_INVALID, "bad n_expert / n_attn_layers / n_input_functions");
-  if (c.input_dim + c.theta_dim > D || c.input_dim > D || c.input_func_dim > D || c.out_dim > D ||
-      c.n_expert > D || c.input_dim < 1 || c.out_dim < 1)
+  if (c.input_dim + c.theta_dim > Dr || c.input_dim > Dr || c.input_func_dim > Dr || c.out_dim > Dr ||
+      c.n_expert > Dr || c.input_dim < 1 || c.out_dim < 1)
     return fail(GNOT_E_INVALID, "input/output widths must be in [1, hidden width]");
   gnot_plan* p = new gnot_plan();
   p->c = c;
-  p->D = D; p->H = c.n_head; p->dh = dh; p->E = c.n_expert; p->L = c.n_attn_layers;
+  p->D = D; p->Dr = Dr; p->H = c.n_head; p->dh = dh; p->E = c.n_expert; p->L = c.n_attn_layers;
   p->I = c.n_input_functions; p->KI = std::max(p->I, 1); p->DT = D / 16;
   p->NL = std::max(c.n_mlp_num_layers, 1) + 1;   // MLP(nl) has max(nl,1)+1 Linears (model.py:9-14)
   p->in = c.input_dim; p->th = c.theta_dim; p->F = c.input_func_dim; p->out = c.out_dim;
   const int NL = p->NL;
+  // canonical Linears at the model's width Dr (= named_parameters() shapes)
   auto mlp = [&](int in, int outd) {
-    for (int j = 0; j < NL; ++j) add_linear(p, j == NL - 1 ? outd : D, j == 0 ? in : D);
+    for (int j = 0; j < NL; ++j) add_linear(p, j == NL - 1 ? outd : Dr, j == 0 ? in : Dr);
   };
-  mlp(p->in + p->th, D);                                   // x
+  mlp(p->in + p->th, Dr);                                  // x
   mlp(p->in, p->E);                                        // gating
-  for (int i = 0; i < p->I; ++i) mlp(p->F, D);             // input_func_mlps
+  for (int i = 0; i < p->I; ++i) mlp(p->F, Dr);            // input_func_mlps
   for (int l = 0; l < p->L; ++l) {
-    for (int k = 0; k < 2 + 2 * p->KI; ++k) add_linear(p, D, D);   // cross q, fc_out, keys, values
-    for (int k = 0; k < 4; ++k) add_linear(p, D, D);               // self q, fc_out, key, value
-    for (int e = 0; e < 2 * p->E; ++e) mlp(D, D);                  // ffn1, ffn2 experts
+    for (int k = 0; k < 2 + 2 * p->KI; ++k) add_linear(p, Dr, Dr);   // cross q, fc_out, keys, values
+    for (int k = 0; k < 4; ++k) add_linear(p, Dr, Dr);               // self q, fc_out, key, value
+    for (int e = 0; e < 2 * p->E; ++e) mlp(Dr, Dr);                  // ffn1, ffn2 experts
   }
-  mlp(D, p->out);                                          // out
+  mlp(Dr, p->out);                                         // out
   if ((int)p->lin_o.size() != p->n_lin()) {
     delete p;
     return fail(GNOT_E_INVALID, "internal: linear count mismatch");
@@ -716,7 +726,7 @@ static void build_groups(gnot_plan* p) {
       WgradJob J{};
       J.dz = A + off[b] * lda; J.lddz = lda;
       J.x = Bm + off[b] * ldb; J.ldx = ldb;
-      J.out = D; J.in = D;
+      J.out = p->Dr; J.in = p->Dr;                // H heads of dh (the real width)
       J.dW = state + b * per_state;
       J.db = J.dW;
       J.w = w ? w + off[b] * ldw : nullptr; J.ldw = ldw; J.wdh = dh;
@@ -763,7 +773,7 @@ static void build_groups(gnot_plan* p) {
           WgradJob J{};
           const long o = p->fnoff[i][b];
           J.dz = kv + o * 2 * D; J.lddz = 2 * D; J.x = kv + D + o * 2 * D; J.ldx = 2 * D;
-          J.out = D; J.in = D; J.dW = st + b * per_state; J.db = J.dW; J.wdh = dh;
+          J.out = p->Dr; J.in = p->Dr; J.dW = st + b * per_state; J.db = J.dW; J.wdh = dh;
           J.state_dh = dh; J.diag_only = 1; J.P = (int)(p->fnoff[i][b + 1] - o);
           p->st_fn.jobs.push_back(J);
         }
@@ -808,7 +818,7 @@ static void build_groups(gnot_plan* p) {
       float* dqkv = p->P_(p->dqkv_buf(false));
       WgradGroup& G = p->wg_self[l];
       const float* q1 = p->P_(s + "query1");
-      lin_job(G, p->lin_so(l), dsum, D, p->P_(s + "sres"), D, 0, P);
+      lin_job(G, p->lin_so(l), dsum, D, p->P_(s + "sres"), p->Dr, 0, P);
       lin_job(G, p->lin_sq(l), dqkv, 3 * D, q1, D, 0, P);
       lin_job(G, p->lin_sk(l), dqkv + D, 3 * D, q1, D, 0, P);
       lin_job(G, p->lin_sv(l), dqkv + 2 * D, 3 * D, q1, D, 0, P);
@@ -819,7 +829,7 @@ static void build_groups(gnot_plan* p) {
       float* dqkv = p->P_(p->dqkv_buf(true));
       WgradGroup& G = p->wg_cross[l];
       const float* qin = p->P_(p->block_query(l));
-      lin_job(G, p->lin_co(l), dsum, D, p->P_(s + "cres"), D, 0, P);
+      lin_job(G, p->lin_co(l), dsum, D, p->P_(s + "cres"), p->Dr, 0, P);
       if (I > 0) {
         lin_job(G, p->lin_cq(l), dqkv, D, qin, D, 0, P);   // key/value grads: wg_fnkv
       } else {
@@ -848,7 +858,7 @@ static void build_attn_tables(gnot_plan* p) {
       LinearArgs a{};
       a.nseg = 1; a.X[0] = p->P_("fnenc" + si); a.ldx = D; a.Wp[0] = A.kv[i].p; a.nsum = 1; a.K = D;
       a.bias = pbias + A.bkv[i]; a.Y = p->P_(s + "ckv" + si); a.ldy = 2 * D; a.NO = 2 * D; a.P = (int)p->Q[i];
-      a.epi = EPI_STORE; a.nsoft = D; a.dh = p->dh;
+      a.epi = EPI_STORE; a.nsoft = D; a.dh = p->dh; a.dreal = p->padded() ? p->Dr : 0;
       p->fwd_kv_jobs.push_back(a);
     }
   if (!p->training) return;
@@ -995,6 +1005,9 @@ extern "C" int gnot_plan_set_shard(gnot_plan* p, int rank, int world, int B, con
     p->world = 1; p->rank = 0; p->nglob.clear(); p->comm = gnot_comm{};
     return GNOT_OK;
   }
+  if (p->padded())
+    return fail(GNOT_E_INVALID, "point sharding needs a hidden width the kernels run unpadded (a multiple of 16 up "
+                                "to 192, or 256)");
   if (rank < 0 || rank >= world || B <= 0 || !n_global || !comm->allreduce_sum || !comm->alltoallv)
     return fail(GNOT_E_INVALID, "bad shard arguments");
   p->world = world;
@@ -1137,13 +1150,13 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
       C.add(s + "cq", P * 3 * D, 3 * D);     // q | k | v of the cross module in self mode
     }
     for (int i = 0; i < KI; ++i) C.add(s + "cstate" + std::to_string(i), p->B * per_state, per_state);
-    C.add(s + "cres", P * D, D);
+    C.add(s + "cres", P * D, p->Dr);   // scramble rows: Dr floats per token (attn_forward)
     C.add(s + "a", P * D, D);
     if (tr && !p->moe_recompute) C.add(s + "m1save", E * NL * P * D, D);
     C.add(s + "query1", P * D, D);
     C.add(s + "sq", P * 3 * D, 3 * D);
     C.add(s + "sstate", p->B * per_state, per_state);
-    C.add(s + "sres", P * D, D);
+    C.add(s + "sres", P * D, p->Dr);
     C.add(s + "bb", P * D, D);
     if (tr && !p->moe_recompute) C.add(s + "m2save", E * NL * P * D, D);
     C.add(s + "query2", P * D, D);
@@ -1154,8 +1167,8 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
     C.add("moe_cnt", (P + 127) / 128, 0);
   if (tr && p->moe_recompute && p->L > 0) C.add("mrsave", E * NL * P * D, D);
   if (p->sharded) {                          // scramble exchange scratch: head-major rows / packed peers
-    C.add("xa", P * D, D);
-    C.add("xb", P * D, D);
+    C.add("xa", P * D, p->Dr);
+    C.add("xb", P * D, p->Dr);
   }
   // attention segments
   make_chunks(p->xoff, p->qchunks, p->qchunk_off);
@@ -1167,7 +1180,7 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
     C.add("dquery", P * D, D);
     C.add("dsum0", P * D, D);
     C.add("dsum1", P * D, D);
-    C.add("dres", P * D, D);
+    C.add("dres", P * D, p->Dr);
     C.add("dqkv0", P * 3 * D, 3 * D);
     C.add("dqkv1", P * 3 * D, 3 * D);
     for (int i = 0; i < KI; ++i) {
@@ -1402,6 +1415,11 @@ extern "C" int gnot_plan_bind_workspace_async(gnot_plan* p, void* workspace, siz
     GNOT_CK(hipEventRecord(p->stage_ev[k], s));
     p->stage_used[k] = true;
   }
+  // a padded width: the pad columns of rows that kernels write per head only (the attention backward's
+  // dq / dk / dv, du) are read as exact zeros by the next backward-data products: clear the activation
+  // part of the workspace once per bind (the tables follow it, uploaded after this on the same stream)
+  if (p->padded())
+    GNOT_CK(hipMemsetAsync(p->ws, 0, p->bufs["__tables"].off, static_cast<hipStream_t>(stream)));
   // the fused soft-MoE combine's completion counters start at zero (each launch leaves them at zero)
   if (p->bufs.count("moe_cnt"))
     GNOT_CK(hipMemsetAsync(p->P_("moe_cnt"), 0, ((p->P + 127) / 128) * sizeof(int), static_cast<hipStream_t>(stream)));
@@ -1464,12 +1482,16 @@ struct ProfScope {
   }
 };
 
+// ncol > 0: store only output columns [0, ncol) (a row pitch below NO: the attention's head-major
+// scramble rows of the real width, attn_backward)
 int run_linear(Ctx& c, const float* X, long ldx, int K, const Img& A, const float* bias, float* Y, long ldy,
-               int NO, long P, int epi, int nsoft) {
+               int NO, long P, int epi, int nsoft, int ncol = 0) {
   LinearArgs a{};
   a.nseg = 1; a.X[0] = X; a.Wp[0] = A.p; a.ldx = ldx; a.nsum = 1; a.sum_stride = 0; a.K = K;
   a.bias = bias; a.Y = Y; a.ldy = ldy; a.NO = NO; a.P = (int)P;
   a.epi = epi; a.nsoft = nsoft; a.dh = c.p->dh; a.np = c.p->np;
+  a.dreal = (nsoft > 0 && c.p->padded()) ? c.p->Dr : 0;
+  a.ncol = ncol;
   GNOT_CK(c.p->D == 256 ? launch_linear2(a, c.s) : launch_linear(a, c.p->D, c.s));
   return GNOT_OK;
 }
@@ -1673,7 +1695,9 @@ int attn_forward(Ctx& c, int l, bool cross, const float* q_in, float* res_out, f
     GNOT_CK(launch_attn_apply_fwd(ap, c.s));
   }
   if (p->sharded) GNOT_RUN(shard_exchange(c, p->P_("xb"), res_out, false));   // the scramble, across ranks
-  GNOT_RUN(run_linear(c, res_out, D, D, A.o, pbias + A.bo, out, D, D, P, EPI_STORE, 0));
+  // fc_out over the scramble rows: Dr columns per token (the head-major apply output viewed as rows of
+  // H * dh = Dr floats, model.py:81-83), read zero-filled to the padded width
+  GNOT_RUN(run_linear(c, res_out, p->Dr, p->Dr, A.o, pbias + A.bo, out, D, D, P, EPI_STORE, 0));
   return GNOT_OK;
 }
 
@@ -1693,7 +1717,7 @@ int attn_backward(Ctx& c, int l, bool cross) {
   const int nq = (int)p->qchunks.size();
   GNOT_RUN(guard_write(c, dqkv));
   // fc_out backward-data: dres = dout W_o (token order); sharded: back to this rank's head-major rows
-  GNOT_RUN(run_linear(c, dsum, D, D, p->T_img[lo], nullptr, dres, D, D, P, EPI_STORE, 0));
+  GNOT_RUN(run_linear(c, dsum, D, D, p->T_img[lo], nullptr, dres, p->Dr, D, P, EPI_STORE, 0, p->Dr));
   if (p->sharded) {
     GNOT_RUN(shard_exchange(c, p->P_("xb"), dres, true));
     dres = p->P_("xb");

@@ -51,6 +51,11 @@ struct LinearArgs {
   int nsoft;                         // feature-softmax on output columns [0, nsoft)
   int dh;                            // head width for that softmax
   int np = 3;                        // linear2: operand pieces (3 = bf16x6, 1 = bf16 mode)
+  // padded hidden width (the plan runs a real width dr < D in tiles of D, engine.cpp gnot_plan_create):
+  // output column c with c % D >= dreal is written as 0 (the softmax of a head's features must not leak
+  // into the pad columns, which the next kernels read as exact zeros); 0 = no pad columns
+  int dreal = 0;
+  int ncol = 0;                      // store only output columns [0, ncol) (row pitch ldy < NO); 0 = all NO
 };
 hipError_t launch_linear(const LinearArgs& a, int D, hipStream_t s);
 // output tiles per workgroup of linear.hip for an NO-column projection with a softmax epilogue over its

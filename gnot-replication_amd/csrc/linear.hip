@@ -62,16 +62,26 @@ GNOT_DEV void linear_body(const LinearArgs& a, float4* wlds) {
   float h[OC][4];
   acc_to_regs<OC>(acc, h);
   if (c * 16 * OC < a.nsoft) softmax_heads<OC>(h, a.dh, lane >> 4);
+  if (a.dreal > 0) {
+    // pad columns of a padded width (D is the tile width; features dreal .. D-1 of each D-block)
+#pragma unroll
+    for (int T = 0; T < OC; ++T)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if ((c * 16 * OC + 16 * T + 4 * (lane >> 4) + r) % D >= a.dreal) h[T][r] = 0.f;
+  }
+  const int ncols = a.ncol > 0 ? min(16 * OC, a.ncol - c * 16 * OC) : 16 * OC;
+  if (ncols <= 0) return;
   float* Y = a.Y + c * 16 * OC;
   if (a.epi == EPI_ACCUM) {
     float old[OC][4];
-    load_rows<OC>(old, Y, a.ldy, p, valid, 16 * OC, lane);
+    load_rows<OC>(old, Y, a.ldy, p, valid, ncols, lane);
 #pragma unroll
     for (int T = 0; T < OC; ++T)
 #pragma unroll
       for (int r = 0; r < 4; ++r) h[T][r] += old[T][r];
   }
-  store_rows<OC>(h, Y, a.ldy, p, valid, 16 * OC, lane);
+  store_rows<OC>(h, Y, a.ldy, p, valid, ncols, lane);
 }
 
 template <int D, int OC>
@@ -105,8 +115,10 @@ int linear_oc(int D, int NO, int nsoft, int dh) {
   }();
   const int kt = D / 16;
   auto ok = [&](int oc) {
+    // the whole row (oc == kt) always keeps whole heads, also at a padded width (D % dh != 0: the heads
+    // tile the first dr features, the pad columns after them are zeroed, LinearArgs::dreal)
     return oc >= 1 && (oc <= 8 || oc == kt) && kt % oc == 0 && NO % (16 * oc) == 0 &&
-           (nsoft == 0 || (16 * oc) % dh == 0);
+           (nsoft == 0 || (16 * oc) % dh == 0 || oc == kt);
   };
   int want = env > 0 ? env : 4;
   if (ok(want)) return want;

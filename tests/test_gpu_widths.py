@@ -1,6 +1,7 @@
 """Hidden and head widths beyond the BASELINE configs: the reference accepts any n_embed divisible by
-n_head (model.py:41).  This core takes every hidden width d that is a multiple of 16 up to 192 (the
-chain.hip / linear.hip kernels, whole 16-wide MFMA tiles) and d = 256 (chain2.hip / linear2.hip), with
+n_head (model.py:41).  This core takes every hidden width d up to 192 (the chain.hip / linear.hip
+kernels, whole 16-wide MFMA tiles; a d that is not a multiple of 16 runs padded to the next one with
+exact-zero pad columns) and d = 256 (chain2.hip / linear2.hip), with
 any head width dh = d / H that is a multiple of 4 up to 64 (the attention passes split a head into
 4-aligned lane slices; the projections' feature softmax reduces a head that straddles 16-feature tiles
 across the 4 lane groups of a point, gnot_common.h softmax_heads).
@@ -36,6 +37,11 @@ CASES = {
     "d160_h8": _cfg(160, 8, 2, 1),        # dh 20
     "d192_h8": _cfg(192, 8, 2, 0),        # dh 24, self-attention only
     "d192_h6": _cfg(192, 6, 2, 1, nl=4),  # dh 32 (fp32-MFMA attention forms at d = 192)
+    # widths that are not a multiple of 16 run padded to the next one (engine.cpp gnot_plan_create: zero pad
+    # columns, the feature softmax's pad columns zeroed, the scramble rows at the real width)
+    "d36_h3": _cfg(36, 3, 2, 1),          # dh 12, kernels at d = 48
+    "d100_h5": _cfg(100, 5, 3, 2, L=2),   # dh 20, kernels at d = 112, two input functions, two blocks
+    "d60_h15": _cfg(60, 15, 2, 0),        # dh 4, kernels at d = 64, self-attention (fused q|k|v) only
 }
 
 

@@ -110,6 +110,34 @@ def test_plan_rejects_bad_config_and_batch():
         lib.gnot_plan_destroy(plan)
 
 
+def test_padded_widths():
+    """A hidden width that is not a multiple of 16 (up to 192) runs on the next multiple's kernels: the
+    plan accepts it, its canonical Linears keep the model's width (the parameter shapes), and point
+    sharding refuses it; head widths must stay multiples of 4 up to 64, and d in (192, 256) is refused."""
+    from gnot_amd import _lib
+    lib = _lib.load()
+    base = dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=1, n_mlp_num_layers=2,
+                n_expert=2, n_input_functions=1)
+    plan = ctypes.c_void_p()
+    for d, H, ok in ((36, 3, True), (100, 5, True), (60, 15, True), (100, 4, False), (200, 5, False),
+                     (208, 13, False), (184, 2, False)):
+        cfg = _lib.GnotConfig(**base, n_attn_hidden_dim=d, n_mlp_hidden_dim=d, n_input_hidden_dim=d, n_head=H)
+        rc = lib.gnot_plan_create(ctypes.byref(cfg), ctypes.byref(plan))
+        assert (rc == 0) == ok, (d, H, rc)
+        if not ok:
+            continue
+        try:
+            n = lib.gnot_plan_num_linears(plan)
+            dims = (ctypes.c_int32 * (2 * n))()
+            _lib.check(lib.gnot_plan_linear_dims(plan, dims))
+            assert max(dims) == d                  # every hidden Linear is d x d (no pad in the parameters)
+            comm = _lib.GnotComm()
+            n_glob = (ctypes.c_int64 * 1)(1000)
+            assert lib.gnot_plan_set_shard(plan, 0, 2, 1, n_glob, ctypes.byref(comm)) == -1
+        finally:
+            lib.gnot_plan_destroy(plan)
+
+
 def test_plan_accepts_meshes_past_the_old_32bit_offset_limit():
     """The streaming kernels base their buffer resources per workgroup / per split-K range (64-bit base,
     32-bit in-tile offsets), so a plan takes configs[4]'s ~1.6M points and configs[3]'s 1M-point mesh at
