@@ -298,18 +298,20 @@ extern "C" int gnot_plan_create(const gnot_config* cfg, gnot_plan** out) {
   // chain.hip / linear.hip run any multiple of 16 up to 192 (whole 16-wide MFMA tiles, activations in
   // registers), chain2.hip / linear2.hip d = 256; the attention passes any head width that is a multiple
   // of 4 up to 64 (4-aligned lane slices, attn.hip; the fp32-MFMA forms at 16 / 32 / 64).  A width below
-  // 192 that is not a multiple of 16 runs padded to the next multiple (Dr real columns + zero pads)
+  // 192 that is not a multiple of 16 runs padded to the next multiple, one in (192, 256) padded to 256
+  // (Dr real columns + zero pads)
   int D = Dr;
   if (Dr % 16 != 0 && Dr < 192) D = (Dr + 15) / 16 * 16;
+  else if (Dr > 192 && Dr < 256) D = 256;            // chain2.hip / linear2.hip with pad columns
   if (!((D % 16 == 0 && D >= 16 && D <= 192) || D == 256))
-    return fail(GNOT_E_INVALID, "hidden width must be at most 192, or 256, on the MI355X kernels");
+    return fail(GNOT_E_INVALID, "hidden width must be at most 256 on the MI355X kernels");
   if (dh % 4 != 0 || dh > 64)
     return fail(GNOT_E_INVALID, "head width d/n_head must be a multiple of 4 up to 64 on the MI355X kernels");
   // the projections' fused feature softmax needs whole heads per workgroup: linear2.hip (d = 256) takes
   // dh = 16 / 32 / 64; linear.hip (the d <= 192 projections and the batched input-function K/V at any d)
   // a tiling of whole heads (linear_oc)
   if (D == 256 && dh != 16 && dh != 32 && dh != 64)
-    return fail(GNOT_E_INVALID, "at hidden width 256 the head width must be 16, 32 or 64 on the MI355X kernels");
+    return fail(GNOT_E_INVALID, "above hidden width 192 the head width must be 16, 32 or 64 on the MI355X kernels");
   if ((D != 256 && (linear_oc(D, 3 * D, 2 * D, dh) < 0 || linear_oc(D, D, D, dh) < 0)) || linear_oc(D, 2 * D, 1, dh) < 0)
     return fail(GNOT_E_INVALID, "no projection tiling keeps whole heads of this head width on the MI355X kernels");
   if (c.n_expert < 1 || c.n_attn_layers < 0 || c.n_input_functions < 0 || c.n_input_functions > 8)

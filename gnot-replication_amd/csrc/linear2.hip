@@ -46,7 +46,8 @@ __global__ void __launch_bounds__(64 * kC2Waves) linear2_kernel(LinearArgs a) {
     for (int k = 0; k < TPH; ++k) {
       bc[k] = bn[k];
       if (a.bias && o0 + TPH < OT) bn[k] = ld4(a.bias + 16 * (o0 + TPH + k) + 4 * g);
-      if (a.epi == EPI_ACCUM) old[k] = ld4(a.Y + pc * a.ldy + 16 * (o0 + k) + 4 * g);
+      if (a.epi == EPI_ACCUM && !(a.ncol > 0 && 16 * (o0 + k) + 4 * g >= a.ncol))
+        old[k] = ld4(a.Y + pc * a.ldy + 16 * (o0 + k) + 4 * g);
     }
 #pragma unroll
     for (int k = 0; k < TPH; ++k) {
@@ -76,12 +77,21 @@ __global__ void __launch_bounds__(64 * kC2Waves) linear2_kernel(LinearArgs a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) h[k][r] *= inv;
     }
+    if (a.dreal > 0) {
+      // pad columns of a padded width (LinearArgs::dreal; whole heads of 16 / 32 / 64 features, so the
+      // pad columns are whole tiles of each 256-column block)
+#pragma unroll
+      for (int k = 0; k < TPH; ++k)
+        if ((16 * (o0 + k)) % 256 >= a.dreal) h[k][0] = h[k][1] = h[k][2] = h[k][3] = 0.f;
+    }
     if (valid) {
 #pragma unroll
       for (int k = 0; k < TPH; ++k) {
+        const int f = 16 * (o0 + k) + 4 * g;
+        if (a.ncol > 0 && f >= a.ncol) continue;     // a row pitch below NO (ncol a multiple of 4)
         float4 v = make_float4(h[k][0], h[k][1], h[k][2], h[k][3]);
         if (a.epi == EPI_ACCUM) { v.x += old[k].x; v.y += old[k].y; v.z += old[k].z; v.w += old[k].w; }
-        *reinterpret_cast<float4*>(a.Y + p * a.ldy + 16 * (o0 + k) + 4 * g) = v;
+        *reinterpret_cast<float4*>(a.Y + p * a.ldy + f) = v;
       }
     }
   }
@@ -137,8 +147,10 @@ __global__ void __launch_bounds__(64 * kC2Waves) linear2_seg_kernel(LinearArgs a
 }
 
 bool linear2_supported(const LinearArgs& a, int D) {
-  return D == 256 && a.K == 256 && a.nsum == 1 && a.NO % 16 == 0 && (a.ldx & 3) == 0 && (a.ldy & 3) == 0 &&
-         (a.nseg == 1 ? (a.nsoft == 0 || a.dh == 16 || a.dh == 32 || a.dh == 64) : (a.NO == 256 && a.nsoft == 0));
+  // K < 256: the input rows are read zero-filled past K (a padded width's scramble rows)
+  return D == 256 && a.K >= 1 && a.K <= 256 && a.nsum == 1 && a.NO % 16 == 0 && (a.ldx & 3) == 0 &&
+         (a.ldy & 3) == 0 && (a.ncol & 3) == 0 && (a.dreal & 15) == 0 &&
+         (a.nseg == 1 ? (a.nsoft == 0 || a.dh == 16 || a.dh == 32 || a.dh == 64) : (a.NO == 256 && a.nsoft == 0 && a.ncol == 0));
 }
 
 template <int NP>

@@ -1,7 +1,7 @@
 """Hidden and head widths beyond the BASELINE configs: the reference accepts any n_embed divisible by
 n_head (model.py:41).  This core takes every hidden width d up to 192 (the chain.hip / linear.hip
 kernels, whole 16-wide MFMA tiles; a d that is not a multiple of 16 runs padded to the next one with
-exact-zero pad columns) and d = 256 (chain2.hip / linear2.hip), with
+exact-zero pad columns) and d = 256 (chain2.hip / linear2.hip; d in (192, 256) padded to it), with
 any head width dh = d / H that is a multiple of 4 up to 64 (the attention passes split a head into
 4-aligned lane slices; the projections' feature softmax reduces a head that straddles 16-feature tiles
 across the 4 lane groups of a point, gnot_common.h softmax_heads).
@@ -42,6 +42,8 @@ CASES = {
     "d36_h3": _cfg(36, 3, 2, 1),          # dh 12, kernels at d = 48
     "d100_h5": _cfg(100, 5, 3, 2, L=2),   # dh 20, kernels at d = 112, two input functions, two blocks
     "d60_h15": _cfg(60, 15, 2, 0),        # dh 4, kernels at d = 64, self-attention (fused q|k|v) only
+    "d208_h13": _cfg(208, 13, 2, 1),      # dh 16, the d = 256 kernels (chain2 / linear2 / wide wgrad) padded
+    "d224_h7": _cfg(224, 7, 3, 0),        # dh 32, d = 256 kernels, self-attention only
 }
 
 
@@ -60,3 +62,23 @@ def test_width_vs_oracle(name, attn_path):
     out, grads = run_packed(m, fx, G)
     errs = check_parity(out, grads, fx)
     assert not errs, errs
+
+
+@pytest.mark.parametrize("name", ["d208_h13", "d224_h7"])
+def test_padded_256_width_bf16_mode(name):
+    """bf16 mode (one RNE bf16 piece per MFMA operand, bf16 storage of the soft-MoE chains) on a width
+    padded to the d = 256 kernels: north_star's 1e-2 norm-wise against the fp64 oracle (tests/test_gpu_bf16.py
+    bar), and really a different arithmetic from the fp32 result."""
+    import numpy as np
+    fx, G = _case(name)
+    m = build_model(fx["params"], fx["cfg"])
+    out32, g32 = run_packed(m, fx, G)
+    m.set_precision("bf16")
+    m.zero_grad(set_to_none=True)
+    out16, g16 = run_packed(m, fx, G)
+    keys = list(fx["grads"].keys())
+    cat = lambda g: np.concatenate([g[k].ravel() for k in keys])
+    rel = lambda a, b: float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+    e_out, e_grad = rel(out16, fx["out"]), rel(cat(g16), cat(fx["grads"]))
+    assert e_out < 1e-2 and e_grad < 1e-2, (e_out, e_grad)
+    assert rel(out16, out32) > 1e-6
