@@ -28,8 +28,11 @@ namespace gnot {
 // In-step (r03x): bf16x6 lead 1 / 2 / 3 = 232.2 / 235.0 / 234.7 ms per configs[2] step (the concurrent
 // weight gradients take the slack); the one-piece bf16 chains lead 3 (a tile's MFMA work is far shorter
 // than a chunk's L2 -> LDS latency)
+#ifndef GNOT_EXP_C2B_LEAD_X6
+#define GNOT_EXP_C2B_LEAD_X6 1
+#endif
 template <int NP>
-constexpr int c2b_lead() { return NP == 3 ? 1 : 3; }
+constexpr int c2b_lead() { return NP == 3 ? GNOT_EXP_C2B_LEAD_X6 : 3; }
 // output tiles per weight chunk of the backward: two in the bf16-storage chains (one counted wait and
 // barrier per pair; the ring buffers of the one-piece chains already hold two tiles, C2Lds::WB)
 template <int NP, bool B16>
@@ -286,8 +289,14 @@ GNOT_DEV void c2f_layer(C2Pipe& pp, const u32x4* W, const u32x4 (&in)[KBI][NP], 
   // which this wave issued the save stores of the epilogues inside tiles o-2 (if o-2 > 0) and o-1
 #pragma unroll
   for (int o = 0; o < OT; o += 2) {
+#ifdef GNOT_DIAG_STAMP
+    const unsigned long long t0 = pp.stamp_in();
+#endif
     if (o == 0) c2_sync_n(pend0);
     else c2_sync_n(SAVE ? (o >= 4 ? 2 : 1) : 0);
+#ifdef GNOT_DIAG_STAMP
+    pp.stamp_out(t0);
+#endif
     const u32x4* cb = pp.cur();
     u32x4* nb = pp.nxt();
     ++pp.cnt;
@@ -328,8 +337,14 @@ GNOT_DEV void c2f_layer(C2Pipe& pp, const u32x4* W, const u32x4 (&in)[KBI][NP], 
   }
 #pragma unroll
   for (int o = 0; o < OT; ++o) {
+#ifdef GNOT_DIAG_STAMP
+    const unsigned long long t0 = pp.stamp_in();
+#endif
     if (o == 0) c2_sync_n(pend0);
     else c2_sync_n((SAVE && o >= 2) ? 1 : 0);
+#ifdef GNOT_DIAG_STAMP
+    pp.stamp_out(t0);
+#endif
     const u32x4* cb = pp.cur();
     u32x4* nb = pp.nxt();
     ++pp.cnt;
@@ -534,6 +549,12 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) 
     if (a.combine != nullptr)
       moe_combine_last<B16>(a.Y, a.y_chain_stride, a.nchains, a.base, a.combine, a.counters, blk, row0, nrows);
   }
+#ifdef GNOT_DIAG_STAMP
+  if (a.dbg && lane == 0) {
+    unsigned long long* d = a.dbg + ((size_t)(blockIdx.x + (size_t)blockIdx.y * gridDim.x) * kC2Waves + wave) * 3;
+    d[0] = pp.ts_body; d[1] = pp.ts_sync; d[2] = pp.ts_n;
+  }
+#endif
 }
 
 // ------------------------------------------------------------------------------------------ backward
@@ -603,7 +624,15 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP],
     // the wait and the weight DMA at the chunk's first tile only
     const int c = o / CH;
     const bool first = o % CH == 0;
-    if (first) c2_sync_n(pp.issued - pp.mark[c % kC2Ring]);
+    if (first) {
+#ifdef GNOT_DIAG_STAMP
+      const unsigned long long t0 = pp.stamp_in();
+#endif
+      c2_sync_n(pp.issued - pp.mark[c % kC2Ring]);
+#ifdef GNOT_DIAG_STAMP
+      pp.stamp_out(t0);
+#endif
+    }
     const u32x4* cb = pp.lds + (c % kC2Ring) * pp.WB + (o % CH) * TU;
     u32x4* nb = pp.lds + ((c + LEAD) % kC2Ring) * pp.WB;
     const int nmark = (c + LEAD) % kC2Ring;
@@ -836,6 +865,12 @@ __global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) 
     if (a.combine != nullptr)
       moe_combine_last<B16>(a.dX, a.dx_chain_stride, a.nchains, nullptr, a.combine, a.counters, blk, row0, nrows);
   }
+#ifdef GNOT_DIAG_STAMP
+  if (a.dbg && lane == 0) {
+    unsigned long long* d = a.dbg + ((size_t)(blockIdx.x + (size_t)blockIdx.y * gridDim.x) * kC2Waves + wave) * 3;
+    d[0] = pp.ts_body; d[1] = pp.ts_sync; d[2] = pp.ts_n;
+  }
+#endif
 }
 
 template <int D, int NP>

@@ -107,6 +107,9 @@ struct ChainArgs {
   // int per 128-point block, zero between launches (each launch's last workgroups reset theirs)
   float* combine = nullptr;
   int* counters = nullptr;
+#ifdef GNOT_DIAG_STAMP
+  unsigned long long* dbg = nullptr;  // diagnostic builds: per-wave stamp sums (x6_core.h C2Pipe)
+#endif
   int grid_mode = 0;                 // set by the launcher (chain2.hip c2_grid_pos)
   // CH_MOE, d = 256, np = 1 (bf16 mode): bf16 activation storage.  Saves and dZ are bf16 "pair-
   // interleaved" rows (gnot_common.h, 512 B per point; strides above then count 4-byte units, so a

@@ -46,6 +46,31 @@ static double time_us(F&& f, int reps = 50) {
   return ms * 1e3 / reps;
 }
 
+#ifdef GNOT_DIAG_STAMP
+// diagnostic build (make microbench EXTRA=-DGNOT_DIAG_STAMP): one extra launch with ChainArgs::dbg set;
+// per wave the shader-clock ticks spent in the chunk waits + barriers (sync) and between them (body)
+static void stamp_report(const char* name, ChainArgs a, bool bwd) {
+  static unsigned long long* dbg = nullptr;
+  const size_t n = (size_t)65536 * 8 * 3;
+  if (!dbg) CK(hipMalloc(&dbg, n * sizeof(unsigned long long)));
+  CK(hipMemset(dbg, 0, n * sizeof(unsigned long long)));
+  a.dbg = dbg;
+  CK(bwd ? launch_chain_bwd(a, nullptr) : launch_chain_fwd(a, nullptr));
+  CK(hipDeviceSynchronize());
+  std::vector<unsigned long long> h(n);
+  CK(hipMemcpy(h.data(), dbg, n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  double body = 0, sync = 0, cnt = 0, waves = 0;
+  for (size_t i = 0; i < n; i += 3)
+    if (h[i + 2]) { body += (double)h[i]; sync += (double)h[i + 1]; cnt += (double)h[i + 2]; waves += 1; }
+  std::printf("stamp %-28s waves %8.0f  syncs/wave %6.1f  sync share %5.3f  ticks/sync %7.1f  body ticks/interval %8.1f\n",
+              name, waves, cnt / std::max(waves, 1.0), sync / std::max(body + sync, 1.0), sync / std::max(cnt, 1.0),
+              body / std::max(cnt - waves, 1.0));
+}
+#define STAMP(name, args, bwd) stamp_report(name, args, bwd)
+#else
+#define STAMP(name, args, bwd) (void)0
+#endif
+
 int main(int argc, char** argv) {
   const int P = argc > 1 ? std::atoi(argv[1]) : 10000;
   const int D = argc > 2 ? std::atoi(argv[2]) : 128;
@@ -81,11 +106,13 @@ int main(int argc, char** argv) {
   std::printf("moe_combine E=%d P=%d D=%d: %8.2f us  %6.0f GB/s\n", E, P, D, t, (E + 2.0) * P * D * 4 / t / 1e3);
   t = time_us([&] { CK(launch_chain_fwd(a, nullptr)); });
   std::printf("chain_fwd  MoE E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
+  STAMP("chain_fwd MoE x6", a, false);
   ChainArgs bw = a;
   bw.dY = X; bw.lddy = D; bw.dscore = dscore; bw.dz = dz; bw.dz_layer_stride = (long)P * D;
   bw.dz_chain_stride = (long)NL * P * D; bw.dX = dX; bw.lddx = D; bw.dx_chain_stride = (long)P * D;
   t = time_us([&] { CK(launch_chain_bwd(bw, nullptr)); });
   std::printf("chain_bwd  MoE E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
+  STAMP("chain_bwd MoE x6", bw, true);
   if (D == 256) {   // the fused soft-MoE combine (counters zero between launches)
     int* cnt = nullptr;
     CK(hipMalloc(&cnt, ((P + 127) / 128) * sizeof(int)));
@@ -128,8 +155,10 @@ int main(int argc, char** argv) {
     bf.combine = qout; bf.counters = cnt;
     t = time_us([&] { CK(launch_chain_fwd(af, nullptr)); });
     std::printf("chain_fwd  b16s+combine E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
+    STAMP("chain_fwd b16s+combine", af, false);
     t = time_us([&] { CK(launch_chain_bwd(bf, nullptr)); });
     std::printf("chain_bwd  b16s+combine E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
+    STAMP("chain_bwd b16s+combine", bf, true);
     CK(hipFree(qout));
     CK(hipFree(cnt));
   }

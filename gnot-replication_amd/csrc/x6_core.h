@@ -174,6 +174,17 @@ GNOT_DEV void c2_sync_n(int n) {   // n is wave-uniform and small
 // counts this wave's vector-memory ops as they are issued, mark[b] is that count right after the DMA of
 // the chunk in buffer b, so issued - mark[b] ops are younger than it
 constexpr int kC2Ring = 4;
+#ifdef GNOT_DIAG_STAMP
+// DIAGNOSTIC builds only (lib/microbench_st): in-kernel clock stamps around the chain kernels' per-chunk
+// wait + barrier (cdna_hip_programming.md section 7, In-kernel stamps); sums leave through ChainArgs::dbg
+GNOT_DEV unsigned long long c2_stamp() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#endif
 struct C2Pipe {
   u32x4* lds;
   int WB;
@@ -181,6 +192,19 @@ struct C2Pipe {
   int wave, lane;
   int issued = 0;
   int mark[kC2Ring] = {0, 0, 0, 0};
+#ifdef GNOT_DIAG_STAMP
+  unsigned long long ts_body = 0, ts_sync = 0, ts_n = 0, ts_last = 0;
+  GNOT_DEV unsigned long long stamp_in() {
+    const unsigned long long t = c2_stamp();
+    if (ts_last) ts_body += t - ts_last;
+    return t;
+  }
+  GNOT_DEV void stamp_out(unsigned long long t0) {
+    ts_last = c2_stamp();
+    ts_sync += ts_last - t0;
+    ++ts_n;
+  }
+#endif
   GNOT_DEV const u32x4* cur() const { return lds + (cnt % kC2Ring) * WB; }
   GNOT_DEV u32x4* nxt() const { return lds + ((cnt + 1) % kC2Ring) * WB; }
 };
