@@ -28,11 +28,11 @@ namespace gnot {
 // In-step (r03x): bf16x6 lead 1 / 2 / 3 = 232.2 / 235.0 / 234.7 ms per configs[2] step (the concurrent
 // weight gradients take the slack); the one-piece bf16 chains lead 3 (a tile's MFMA work is far shorter
 // than a chunk's L2 -> LDS latency)
-#ifndef GNOT_EXP_C2B_LEAD_X6
-#define GNOT_EXP_C2B_LEAD_X6 1
-#endif
+// Round 4 (no concurrent weight gradients, microbench r04ld, one box): bf16x6 lead 2 / 3 = 8.39 / 8.42 ms
+// against 8.26-8.29 for lead 1, with the wait + barrier share of the tile unchanged at 0.30 (stamp build):
+// the wait is the barrier's skew between the 8 waves, not the chunk's latency
 template <int NP>
-constexpr int c2b_lead() { return NP == 3 ? GNOT_EXP_C2B_LEAD_X6 : 3; }
+constexpr int c2b_lead() { return NP == 3 ? 1 : 3; }
 // output tiles per weight chunk of the backward: two in the bf16-storage chains (one counted wait and
 // barrier per pair; the ring buffers of the one-piece chains already hold two tiles, C2Lds::WB)
 template <int NP, bool B16>
@@ -149,14 +149,15 @@ GNOT_DEV void moe_combine_last(const float* stage, long stage_stride, int E, con
     const unsigned bytes = (unsigned)nrows * 1024u, sbytes = (unsigned)nrows * (unsigned)kB16Row;
     const rsrc_t ro = make_rsrc(out + fo, bytes);
     const rsrc_t rb = make_rsrc(base ? base + fo : out + fo, base ? bytes : 0u);
+    constexpr int RS = 2 * kC2Waves;              // rows per step (threads / 32)
     const int t = threadIdx.x, ch = t & 31, r0 = t >> 5;
     const int f0 = 32 * (ch >> 2) + 4 * (ch & 3);   // first feature of half 0 (half 1: + 16)
-    for (int k = 0; k < 8; k += R) {
+    for (int k = 0; k < kC2Rows / RS; k += R) {
       int vo[R], vs[R];
       float4 lo[R], hi[R];
 #pragma unroll
       for (int i = 0; i < R; ++i) {
-        const int row = r0 + 16 * (k + i);
+        const int row = r0 + RS * (k + i);
         vo[i] = row * 1024 + f0 * 4;
         vs[i] = row * kB16Row + ch * 16;
         lo[i] = base ? buf_load_f32x4(rb, vo[i], 0) : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -201,12 +202,12 @@ GNOT_DEV void moe_combine_last(const float* stage, long stage_stride, int E, con
   const rsrc_t ro = make_rsrc(out + fo, bytes);
   const rsrc_t rb = make_rsrc(base ? base + fo : out + fo, base ? bytes : 0u);
   const int t = threadIdx.x, c16 = (t & 63) * 16, r0 = t >> 6;
-  for (int k = 0; k < 16; k += R) {
+  for (int k = 0; k < kC2Rows / kC2Waves; k += R) {
     int vo[R];
     float4 acc[R];
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      vo[i] = (r0 + 8 * (k + i)) * 1024 + c16;
+      vo[i] = (r0 + kC2Waves * (k + i)) * 1024 + c16;
       acc[i] = base ? buf_load_f32x4(rb, vo[i], 0) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     for (int e0 = 0; e0 < E; e0 += 8) {
@@ -382,7 +383,7 @@ GNOT_DEV void c2f_layer(C2Pipe& pp, const u32x4* W, const u32x4 (&in)[KBI][NP], 
 // B16 (bf16 mode, ChainArgs::b16s): bf16 pair-interleaved saves, plus each Linear's RNE bf16 input (the
 // split the MFMAs consume, stored as it is made) for the weight gradients
 template <int D, int KT0, int OTL, bool SAVE, int NP, bool WALK, bool B16 = false>
-__global__ void __launch_bounds__(64 * kC2Waves) chain2_fwd_kernel(ChainArgs a) {
+__global__ void __launch_bounds__(64 * kC2Waves, 2) chain2_fwd_kernel(ChainArgs a) {
   constexpr int DT = D / 16, KB = DT / 2, KB0 = (KT0 + 1) / 2;
   using LD = C2Lds<D, NP>;
   extern __shared__ __attribute__((aligned(16))) u32x4 c2lds[];
@@ -695,7 +696,7 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP],
 // in place (expert e > 0 reads back the partial this lane stored for e-1), no stage, no combine pass.
 // B16 (bf16 mode, ChainArgs::b16s): saves and dz as bf16 pair-interleaved rows
 template <int D, int KT0, int OTL, int NP, bool WALK, bool B16 = false>
-__global__ void __launch_bounds__(64 * kC2Waves) chain2_bwd_kernel(ChainArgs a) {
+__global__ void __launch_bounds__(64 * kC2Waves, 2) chain2_bwd_kernel(ChainArgs a) {
   constexpr int DT = D / 16, KB = DT / 2, KBL = (OTL + 1) / 2;
   using LD = C2Lds<D, NP>;
   extern __shared__ __attribute__((aligned(16))) u32x4 c2lds[];

@@ -1166,7 +1166,7 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
   p->moe_walk = p->D == 256 && p->L > 0 && chain2_walk_choice(P, E);
   if (!p->moe_walk) C.add("stage", E * P * D, D);
   if (p->D == 256 && p->L > 0 && !p->moe_walk)        // fused-combine completion counters, one per 128 points
-    C.add("moe_cnt", (P + 127) / 128, 0);
+    C.add("moe_cnt", (P + kC2Rows - 1) / kC2Rows, 0);
   if (tr && p->moe_recompute && p->L > 0) C.add("mrsave", E * NL * P * D, D);
   if (p->sharded) {                          // scramble exchange scratch: head-major rows / packed peers
     C.add("xa", P * D, p->Dr);
@@ -1424,7 +1424,7 @@ extern "C" int gnot_plan_bind_workspace_async(gnot_plan* p, void* workspace, siz
     GNOT_CK(hipMemsetAsync(p->ws, 0, p->bufs["__tables"].off, static_cast<hipStream_t>(stream)));
   // the fused soft-MoE combine's completion counters start at zero (each launch leaves them at zero)
   if (p->bufs.count("moe_cnt"))
-    GNOT_CK(hipMemsetAsync(p->P_("moe_cnt"), 0, ((p->P + 127) / 128) * sizeof(int), static_cast<hipStream_t>(stream)));
+    GNOT_CK(hipMemsetAsync(p->P_("moe_cnt"), 0, ((p->P + kC2Rows - 1) / kC2Rows) * sizeof(int), static_cast<hipStream_t>(stream)));
   if (!p->side2) GNOT_CK(hipStreamCreateWithFlags(&p->side2, hipStreamNonBlocking));
   if (!p->side) {
     // same priority as the caller's stream: measured on MI355X, a low- (or high-) priority side

@@ -69,6 +69,9 @@ hipError_t launch_linear_batch(const LinearArgs* jobs_dev, int njobs, int maxP, 
 
 // ------------------------------------------------------------------ fused MLP chains (chain.hip)
 enum ChainMode { CH_STORE = 0, CH_SOFTMAX = 1, CH_MOE = 2 };
+// points per workgroup of the d = 256 chain kernels (chain2.hip: 16 per wave): one block of the soft-MoE
+// expert grid, and one fused-combine completion counter
+constexpr int kC2Rows = 128;
 struct ChainLayer {
   const float4* Wp;    // packed forward weights of this layer
   const float4* WpT;   // packed transposed weights (backward)

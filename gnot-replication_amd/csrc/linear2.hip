@@ -16,7 +16,7 @@
 namespace gnot {
 
 template <int TPH, int NP>   // output tiles per softmax head (dh / 16); operand pieces (3 = x6, 1 = bf16)
-__global__ void __launch_bounds__(64 * kC2Waves) linear2_kernel(LinearArgs a) {
+__global__ void __launch_bounds__(64 * kC2Waves, 2) linear2_kernel(LinearArgs a) {
   constexpr int DT = 16, KB = 8;
   extern __shared__ __attribute__((aligned(16))) u32x4 c2lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
@@ -98,7 +98,7 @@ __global__ void __launch_bounds__(64 * kC2Waves) linear2_kernel(LinearArgs a) {
 }
 
 template <int NP>
-__global__ void __launch_bounds__(64 * kC2Waves) linear2_seg_kernel(LinearArgs a) {
+__global__ void __launch_bounds__(64 * kC2Waves, 2) linear2_seg_kernel(LinearArgs a) {
   constexpr int DT = 16, KB = 8;
   extern __shared__ __attribute__((aligned(16))) u32x4 c2lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;

@@ -115,8 +115,8 @@ int main(int argc, char** argv) {
   STAMP("chain_bwd MoE x6", bw, true);
   if (D == 256) {   // the fused soft-MoE combine (counters zero between launches)
     int* cnt = nullptr;
-    CK(hipMalloc(&cnt, ((P + 127) / 128) * sizeof(int)));
-    CK(hipMemset(cnt, 0, ((P + 127) / 128) * sizeof(int)));
+    CK(hipMalloc(&cnt, (size_t)P * sizeof(int)));
+    CK(hipMemset(cnt, 0, (size_t)P * sizeof(int)));
     float* qout = dalloc((size_t)P * D, 0.0f);
     ChainArgs af = a, bf = bw;
     af.base = X; af.combine = qout; af.counters = cnt;
@@ -147,8 +147,8 @@ int main(int argc, char** argv) {
     std::printf("chain_fwd  b16s saves-only E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
     a2.Y = Y;
     int* cnt = nullptr;
-    CK(hipMalloc(&cnt, ((P + 127) / 128) * sizeof(int)));
-    CK(hipMemset(cnt, 0, ((P + 127) / 128) * sizeof(int)));
+    CK(hipMalloc(&cnt, (size_t)P * sizeof(int)));
+    CK(hipMemset(cnt, 0, (size_t)P * sizeof(int)));
     float* qout = dalloc((size_t)P * D, 0.0f);
     ChainArgs af = a2, bf = b2;
     af.base = X; af.combine = qout; af.counters = cnt;

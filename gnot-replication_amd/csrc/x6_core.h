@@ -9,6 +9,7 @@
 namespace gnot {
 
 constexpr int kC2Waves = 8;
+static_assert(kC2Rows == 16 * kC2Waves, "chain workgroup rows (gnot_kernels.h) != 16 points per wave");
 
 // Piece count NP: 3 = the exact bf16x6 form (fp32 arithmetic), 1 = plain bf16 (RNE operands, fp32
 // accumulation: the bf16 arithmetic mode, gnot_plan_set_precision).
@@ -191,7 +192,7 @@ struct C2Pipe {
   int cnt;          // weight chunks consumed (ring position)
   int wave, lane;
   int issued = 0;
-  int mark[kC2Ring] = {0, 0, 0, 0};
+  int mark[kC2Ring] = {};
 #ifdef GNOT_DIAG_STAMP
   unsigned long long ts_body = 0, ts_sync = 0, ts_n = 0, ts_last = 0;
   GNOT_DEV unsigned long long stamp_in() {
