@@ -19,22 +19,31 @@ constexpr int c2_tile_u4(int KB, int NP = 3) { return KB * NP * WAVE; }
 // acc += sum_t W[o][t] . in[t] for one output tile: the weight pieces of k-block t+1 are read from
 // LDS while the MFMAs of block t run (x6: the six order <= 2 products, smallest terms first, one
 // accumulator; bf16: one product)
+// fragment sets in flight: bf16x6 one k-block ahead (its six MFMAs cover the next block's LDS latency);
+// one piece three ahead (a single 16-cycle MFMA per block would leave each read's latency exposed)
+template <int NP, bool AHEAD>
+constexpr int c2_frag_depth() { return AHEAD ? (NP == 1 ? 4 : 2) : 1; }
 template <int KB, bool AHEAD = true, int NP = 3>
 GNOT_DEV f32x4 c2_tile(const u32x4* __restrict__ cb, const u32x4 (&bp)[KB][NP], f32x4 acc, int lane) {
-  u32x4 a[AHEAD ? 2 : 1][NP];
+  constexpr int DP = c2_frag_depth<NP, AHEAD>();
+  u32x4 a[DP][NP];
 #pragma unroll
-  for (int q = 0; q < NP; ++q) a[0][q] = cb[q * WAVE + lane];
+  for (int d = 0; d + 1 < DP || d == 0; ++d)
+    if (d < KB) {
+#pragma unroll
+      for (int q = 0; q < NP; ++q) a[d][q] = cb[(d * NP + q) * WAVE + lane];
+    }
 #pragma unroll
   for (int t = 0; t < KB; ++t) {
     if (!AHEAD && t > 0) {
 #pragma unroll
       for (int q = 0; q < NP; ++q) a[0][q] = cb[(t * NP + q) * WAVE + lane];
     }
-    if (AHEAD && t + 1 < KB) {
+    if (AHEAD && t + DP - 1 < KB) {
 #pragma unroll
-      for (int q = 0; q < NP; ++q) a[(t + 1) & 1][q] = cb[((t + 1) * NP + q) * WAVE + lane];
+      for (int q = 0; q < NP; ++q) a[(t + DP - 1) % DP][q] = cb[((t + DP - 1) * NP + q) * WAVE + lane];
     }
-    const u32x4(&w)[NP] = a[AHEAD ? (t & 1) : 0];
+    const u32x4(&w)[NP] = a[AHEAD ? (t % DP) : 0];
     if constexpr (NP == 3) {
       acc = mfma_bf16(w[2], bp[t][0], acc);
       acc = mfma_bf16(w[1], bp[t][1], acc);
@@ -44,7 +53,7 @@ GNOT_DEV f32x4 c2_tile(const u32x4* __restrict__ cb, const u32x4 (&bp)[KB][NP], 
     }
     acc = mfma_bf16(w[0], bp[t][0], acc);
     if (AHEAD) {
-      if (t + 1 < KB) __builtin_amdgcn_sched_group_barrier(0x100, NP, 0);
+      if (t + DP - 1 < KB) __builtin_amdgcn_sched_group_barrier(0x100, NP, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, NP == 3 ? 6 : 1, 0);
     }
   }
@@ -64,10 +73,15 @@ struct C2NoPre {
 template <int KB, int NP, bool AHEAD, typename Epi, typename Pre = C2NoPre>
 GNOT_DEV f32x4 c2_tile_epi(const u32x4* __restrict__ cb, const u32x4 (&bp)[KB][NP], f32x4 acc, int lane, Epi&& epi,
                            Pre&& pre = Pre()) {
-  u32x4 ab[AHEAD ? 2 : 1][NP];
+  constexpr int DP = c2_frag_depth<NP, AHEAD>();
+  u32x4 ab[DP][NP];
   if (AHEAD) {
 #pragma unroll
-    for (int q = 0; q < NP; ++q) ab[0][q] = cb[q * WAVE + lane];
+    for (int d = 0; d + 1 < DP; ++d)
+      if (d < KB) {
+#pragma unroll
+        for (int q = 0; q < NP; ++q) ab[d][q] = cb[(d * NP + q) * WAVE + lane];
+      }
   }
   __builtin_amdgcn_sched_barrier(0);
   pre();
@@ -75,15 +89,15 @@ GNOT_DEV f32x4 c2_tile_epi(const u32x4* __restrict__ cb, const u32x4 (&bp)[KB][N
 #pragma unroll
   for (int t = 0; t < KB; ++t) {
     if (AHEAD) {
-      if (t + 1 < KB) {
+      if (t + DP - 1 < KB) {
 #pragma unroll
-        for (int q = 0; q < NP; ++q) ab[(t + 1) & 1][q] = cb[((t + 1) * NP + q) * WAVE + lane];
+        for (int q = 0; q < NP; ++q) ab[(t + DP - 1) % DP][q] = cb[((t + DP - 1) * NP + q) * WAVE + lane];
       }
     } else {
 #pragma unroll
       for (int q = 0; q < NP; ++q) ab[0][q] = cb[(t * NP + q) * WAVE + lane];
     }
-    const u32x4(&a)[NP] = ab[AHEAD ? (t & 1) : 0];
+    const u32x4(&a)[NP] = ab[AHEAD ? (t % DP) : 0];
     if constexpr (NP == 3) {
       acc = mfma_bf16(a[2], bp[t][0], acc);
       acc = mfma_bf16(a[1], bp[t][1], acc);
@@ -93,9 +107,9 @@ GNOT_DEV f32x4 c2_tile_epi(const u32x4* __restrict__ cb, const u32x4 (&bp)[KB][N
     }
     acc = mfma_bf16(a[0], bp[t][0], acc);
     if (AHEAD) {
-      // keep block t+1's fragment reads ahead of block t's MFMAs (the scheduler otherwise sinks them
+      // keep the fragment reads DP-1 blocks ahead of block t's MFMAs (the scheduler otherwise sinks them
       // next to their use to save registers, exposing the LDS latency every block)
-      if (t + 1 < KB) __builtin_amdgcn_sched_group_barrier(0x100, NP, 0);
+      if (t + DP - 1 < KB) __builtin_amdgcn_sched_group_barrier(0x100, NP, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, NP == 3 ? 6 : 1, 0);
     }
     if ((t & 1) && (t >> 1) < 4) {
