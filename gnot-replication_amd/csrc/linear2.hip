@@ -15,17 +15,25 @@
 
 namespace gnot {
 
+// waves (16 points each) per workgroup: bf16x6 4 (two workgroups per CU, one's input loads and output
+// stores overlap the other's MFMAs; the 384 KiB x6 image stays L2-resident), one piece 8.  Interleaved on
+// one box (profiles/r04l2w_linear2_waves_ab.txt), 8 -> 4 waves: bf16x6 NO = 256 251 -> 233 us, accumulate
+// 300 -> 266, three K-segments 670 -> 645, NO = 768 585 -> 552; one piece 131 -> 153 and 273 -> 351 (its
+// eight waves already fit two workgroups per CU by registers)
+template <int NP>
+constexpr int l2_waves() { return NP == 3 ? 4 : 8; }
+
 template <int TPH, int NP>   // output tiles per softmax head (dh / 16); operand pieces (3 = x6, 1 = bf16)
-__global__ void __launch_bounds__(64 * kC2Waves, 2) linear2_kernel(LinearArgs a) {
+__global__ void __launch_bounds__(64 * l2_waves<NP>(), 2) linear2_kernel(LinearArgs a) {
   constexpr int DT = 16, KB = 8;
   extern __shared__ __attribute__((aligned(16))) u32x4 c2lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
-  const long p = ((long)blockIdx.x * kC2Waves + wave) * 16 + (lane & 15);
+  const long p = ((long)blockIdx.x * l2_waves<NP>() + wave) * 16 + (lane & 15);
   const bool valid = p < a.P;
   const int OT = a.NO / 16;
   const u32x4* W = reinterpret_cast<const u32x4*>(a.Wp[0]);
-  C2Stream st{c2lds, c2_tile_u4(KB, NP), 0, wave, lane};
-  stage_image(reinterpret_cast<float4*>(c2lds), reinterpret_cast<const float4*>(W), c2_tile_u4(KB, NP), kC2Waves,
+  C2Stream st{c2lds, c2_tile_u4(KB, NP), 0, wave, lane, l2_waves<NP>()};
+  stage_image(reinterpret_cast<float4*>(c2lds), reinterpret_cast<const float4*>(W), c2_tile_u4(KB, NP), l2_waves<NP>(),
               wave, lane);
   u32x4 bp[KB][NP];
   {
@@ -53,7 +61,10 @@ __global__ void __launch_bounds__(64 * kC2Waves, 2) linear2_kernel(LinearArgs a)
     for (int k = 0; k < TPH; ++k) {
       const int o = o0 + k;
       const u32x4* cb = st.begin(W, o, OT, c2_tile_u4(KB, NP), nullptr, 0);
-      const f32x4 acc = c2_tile<KB, true, NP>(cb, bp, f32x4{bc[k].x, bc[k].y, bc[k].z, bc[k].w}, lane);
+      // the epilogue form with no epilogue: its scheduling fences keep k-block t+1's fragment reads ahead
+      // of block t's MFMAs (the plain form compiled to reads issued next to their MFMAs here)
+      const f32x4 acc = c2_tile_epi<KB, NP, true>(cb, bp, f32x4{bc[k].x, bc[k].y, bc[k].z, bc[k].w}, lane,
+                                                  [](int) {});
 #pragma unroll
       for (int r = 0; r < 4; ++r) h[k][r] = acc[r];
     }
@@ -98,15 +109,15 @@ __global__ void __launch_bounds__(64 * kC2Waves, 2) linear2_kernel(LinearArgs a)
 }
 
 template <int NP>
-__global__ void __launch_bounds__(64 * kC2Waves, 2) linear2_seg_kernel(LinearArgs a) {
+__global__ void __launch_bounds__(64 * l2_waves<NP>(), 2) linear2_seg_kernel(LinearArgs a) {
   constexpr int DT = 16, KB = 8;
   extern __shared__ __attribute__((aligned(16))) u32x4 c2lds[];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
-  const long p = ((long)blockIdx.x * kC2Waves + wave) * 16 + (lane & 15);
+  const long p = ((long)blockIdx.x * l2_waves<NP>() + wave) * 16 + (lane & 15);
   const bool valid = p < a.P;
-  C2Stream st{c2lds, c2_tile_u4(KB, NP), 0, wave, lane};
+  C2Stream st{c2lds, c2_tile_u4(KB, NP), 0, wave, lane, l2_waves<NP>()};
   stage_image(reinterpret_cast<float4*>(c2lds), reinterpret_cast<const float4*>(a.Wp[0]), c2_tile_u4(KB, NP),
-              kC2Waves, wave, lane);
+              l2_waves<NP>(), wave, lane);
   f32x4 acc[DT];
 #pragma unroll
   for (int o = 0; o < DT; ++o) {
@@ -129,7 +140,7 @@ __global__ void __launch_bounds__(64 * kC2Waves, 2) linear2_seg_kernel(LinearArg
 #pragma unroll
     for (int o = 0; o < DT; ++o) {
       const u32x4* cb = st.begin(W, o, DT, c2_tile_u4(KB, NP), next, c2_tile_u4(KB, NP));
-      acc[o] = c2_tile<KB, false, NP>(cb, bp, acc[o], lane);
+      acc[o] = c2_tile_epi<KB, NP, true>(cb, bp, acc[o], lane, [](int) {});   // reads one k-block ahead
     }
   }
   if (valid) {
@@ -156,7 +167,7 @@ bool linear2_supported(const LinearArgs& a, int D) {
 template <int NP>
 static hipError_t launch_linear2_np(const LinearArgs& a, hipStream_t s) {
   const size_t lds = 2 * (size_t)c2_tile_u4(8, NP) * 16;
-  const dim3 grid((a.P + 16 * kC2Waves - 1) / (16 * kC2Waves)), block(64 * kC2Waves);
+  const dim3 grid((a.P + 16 * l2_waves<NP>() - 1) / (16 * l2_waves<NP>())), block(64 * l2_waves<NP>());
   static bool attr = false;
   if (!attr) {
     for (const void* f : {reinterpret_cast<const void*>(linear2_kernel<1, NP>), reinterpret_cast<const void*>(linear2_kernel<2, NP>),

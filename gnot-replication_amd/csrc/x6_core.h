@@ -131,6 +131,7 @@ struct C2Stream {
   int buf_u4;
   int cnt = 0;
   int wave, lane;
+  int nwaves = kC2Waves;   // waves of the workgroup sharing the stream
   GNOT_DEV const u32x4* begin(const u32x4* img, int o, int OT, int tile_u4, const u32x4* next, int next_u4) {
     lds_dma_wait();
     __syncthreads();
@@ -139,7 +140,7 @@ struct C2Stream {
     int n = 0;
     if (o + 1 < OT) { src = reinterpret_cast<const float4*>(img + (size_t)(o + 1) * tile_u4); n = tile_u4; }
     else if (next) { src = reinterpret_cast<const float4*>(next); n = next_u4; }
-    if (src) stage_image(reinterpret_cast<float4*>(nb), src, n, kC2Waves, wave, lane);
+    if (src) stage_image(reinterpret_cast<float4*>(nb), src, n, nwaves, wave, lane);
     const u32x4* cb = lds + (cnt & 1) * buf_u4;
     ++cnt;
     return cb;
