@@ -304,8 +304,9 @@ def main():
     backend = os.environ.get("GNOT_BENCH_BACKEND", "nccl")
     if os.environ.get("GNOT_BENCH_ONE_GPU"):
         local = 0
-    # GNOT_BENCH_FORCE_SHARD=1: run the point-shard path (eager, engine callbacks, RCCL collectives) even
-    # at one rank -- the N=1 reference of the sharded step the multi-GPU runs take
+    # GNOT_BENCH_FORCE_SHARD=1: run the point-shard path (engine callbacks, RCCL collectives, the per-group
+    # gradient all-reduce, all captured in the step's hipGraph) even at one rank -- the N=1 reference of
+    # the sharded step the multi-GPU runs take
     force_shard = os.environ.get("GNOT_BENCH_FORCE_SHARD") == "1"
     if world > 1 or force_shard:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -380,7 +381,7 @@ def main():
         comm = par.PointShardComm(stage_via_host=backend != "nccl")
     if shard:
         model.set_point_shard(comm)
-    if world > 1 and os.environ.get("GNOT_BENCH_FLAT_ALLREDUCE") != "1":
+    if (world > 1 or force_shard) and os.environ.get("GNOT_BENCH_FLAT_ALLREDUCE") != "1":
         # the parameter gradients are summed over the ranks INSIDE the backward, one collective per weight-
         # gradient group as soon as it is written (overlapped with the rest of the backward; SURVEY.md
         # section 5); GNOT_BENCH_FLAT_ALLREDUCE=1: one all-reduce of the flat buffer after the backward
