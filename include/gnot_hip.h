@@ -32,7 +32,9 @@ typedef struct gnot_plan gnot_plan; /* opaque */
 
 /* GNOT constructor arguments, reference model.py:143 (positional order of main.py:44).
  * n_attn_hidden_dim, n_mlp_hidden_dim and n_input_hidden_dim must be equal (the reference's
- * residual adds, model.py:131/137, require it); d a multiple of 16 up to 192, or 256; d/n_head a multiple of 4 up to 64. */
+ * residual adds, model.py:131/137, require it); d up to 256 (a d that is not a multiple of 16 up to 192, or 256,
+ * runs on the next of those widths with exact-zero pad columns; parameters, gradients and outputs keep d);
+ * d/n_head a multiple of 4 up to 64, and 16 / 32 / 64 above d = 192. */
 typedef struct gnot_config {
   int input_dim;
   int theta_dim;
@@ -175,7 +177,8 @@ int gnot_plan_set_grad_comm(gnot_plan* plan, const gnot_comm* comm);
 
 /* Declare the rank's shard of the next batch: n_global[b] = points of sample b over all ranks.
  * Call before gnot_plan_set_batch, whose x_off then gives the LOCAL slices (validated against
- * gnot_shard_range).  world == 1 (or comm == NULL) switches sharding off.  `comm` is copied. */
+ * gnot_shard_range).  world == 1 (or comm == NULL) switches sharding off.  `comm` is copied.
+ * A padded hidden width (see gnot_config) is refused (GNOT_E_INVALID). */
 int gnot_plan_set_shard(gnot_plan* plan, int rank, int world, int B, const int64_t* n_global, const gnot_comm* comm);
 
 /* Host-only helpers (no GPU): the canonical point range of a rank, and the rank's side of the
