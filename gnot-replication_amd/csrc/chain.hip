@@ -263,10 +263,10 @@ static hipError_t launch_chain(const ChainArgs& a, bool bwd, hipStream_t s) {
 
 // d = 256 runs on chain2.hip (output-major bf16x6 in both directions; the engine packs its images)
 hipError_t launch_chain_fwd(const ChainArgs& a, hipStream_t s) {
-  return a.D == 256 ? launch_chain2(a, false, s) : launch_chain(a, false, s);
+  return a.D > 256 ? launch_chainw(a, false, s) : a.D == 256 ? launch_chain2(a, false, s) : launch_chain(a, false, s);
 }
 hipError_t launch_chain_bwd(const ChainArgs& a, hipStream_t s) {
-  return a.D == 256 ? launch_chain2(a, true, s) : launch_chain(a, true, s);
+  return a.D > 256 ? launch_chainw(a, true, s) : a.D == 256 ? launch_chain2(a, true, s) : launch_chain(a, true, s);
 }
 
 }  // namespace gnot

@@ -303,8 +303,11 @@ extern "C" int gnot_plan_create(const gnot_config* cfg, gnot_plan** out) {
   int D = Dr;
   if (Dr % 16 != 0 && Dr < 192) D = (Dr + 15) / 16 * 16;
   else if (Dr > 192 && Dr < 256) D = 256;            // chain2.hip / linear2.hip with pad columns
-  if (!((D % 16 == 0 && D >= 16 && D <= 192) || D == 256))
-    return fail(GNOT_E_INVALID, "hidden width must be at most 256 on the MI355X kernels");
+  else if (Dr > 256) D = (Dr + 63) / 64 * 64;         // 320 .. 512: chainw.hip (one Linear at a time)
+  if (!((D % 16 == 0 && D >= 16 && D <= 192) || D == 256 || (D > 256 && D <= 512)))
+    return fail(GNOT_E_INVALID, "hidden width must be at most 512 on the MI355X kernels");
+  if (D > 256 && 64 % dh != 0)
+    return fail(GNOT_E_INVALID, "above hidden width 256 the head width must divide 64 on the MI355X kernels");
   if (dh % 4 != 0 || dh > 64)
     return fail(GNOT_E_INVALID, "head width d/n_head must be a multiple of 4 up to 64 on the MI355X kernels");
   // the projections' fused feature softmax needs whole heads per workgroup: linear2.hip (d = 256) takes
@@ -479,14 +482,16 @@ static void plan_images(gnot_plan* p) {
   const bool c2 = p->D == 256;
   const int c2np = c2 ? p->np : 3;                 // pieces of the output-major images
   const int c2x6 = c2np == 1 ? 3 : 2;              // their pack mode
+  // d > 256 (chainw.hip: each Linear on linear.hip): fp32 fragment images in both directions
+  const bool cw = p->D > 256;
   auto chain_imgs = [&](int first, int KT0, int OTL) {
     for (int j = 0; j < NL; ++j) {
       const int li = first + j;
       const int KTp = (j == 0) ? KT0 : DT;
       const int OTp = (j == NL - 1) ? OTL : DT;
-      Img f = new_img_x6(OTp, KTp, c2np);
+      Img f = cw ? new_img(OTp, KTp) : new_img_x6(OTp, KTp, c2np);
       const size_t bo = new_bias(16 * OTp);
-      job(li, f, 0, 0, OTp, KTp, 0, (long)bo, c2 ? c2x6 : 1);
+      job(li, f, 0, 0, OTp, KTp, 0, (long)bo, cw ? 0 : c2 ? c2x6 : 1);
       Img t = c2 ? new_img_x6(KTp, OTp, c2np) : new_img(KTp, OTp);   // backward-data image
       job(li, t, 0, 0, KTp, OTp, 1, -1, c2 ? c2x6 : 0);
       p->fwd_img[li] = f;
@@ -1165,6 +1170,10 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
   }
   p->moe_walk = p->D == 256 && p->L > 0 && chain2_walk_choice(P, E);
   if (!p->moe_walk) C.add("stage", E * P * D, D);
+  if (D > 256) {                             // chainw.hip scratch: query-branch chains / input-function branch
+    C.add("lw_scr", 2 * P * D, D);
+    if (I > 0) C.add("lw_scr2", 2 * Qmax * D, D);
+  }
   if (p->D == 256 && p->L > 0 && !p->moe_walk)        // fused-combine completion counters, one per 128 points
     C.add("moe_cnt", (P + kC2Rows - 1) / kC2Rows, 0);
   if (tr && p->moe_recompute && p->L > 0) C.add("mrsave", E * NL * P * D, D);
@@ -1514,9 +1523,17 @@ int run_linear_seg(Ctx& c, std::initializer_list<std::pair<const float*, const I
   return GNOT_OK;
 }
 
+// d > 256: the chainw.hip scratch of the stream a chain call runs on (the input-function branch on side2
+// runs concurrently with the query branch)
+ChainArgs& cw_scratch(gnot_plan* p, ChainArgs& a, hipStream_t s) {
+  if (p->D > 256) a.scratch = p->P_(s == p->side2 ? "lw_scr2" : "lw_scr");
+  return a;
+}
+
 ChainArgs chain_args(gnot_plan* p, const ChainTable& T, long P) {
   ChainArgs a{};
   a.D = p->D; a.KT0 = T.KT0; a.OTL = T.OTL; a.nlin = p->NL;
+  a.layers_host = T.host.data();
   a.in_dim = T.in_dim; a.out_dim = T.out_dim; a.P = (int)P; a.nchains = T.nchains; a.layers = T.dev;
   a.np = p->np;
   return a;
@@ -1801,7 +1818,7 @@ static int moe_forward(Ctx& c, const ChainTable& T, const float* in, const float
   }
   {
     ProfScope ps(c, "moe_fwd", 2.0 * E * P * NL * (double)D * D);
-    GNOT_CK(launch_chain_fwd(a, c.s));
+    GNOT_CK(launch_chain_fwd(cw_scratch(p, a, c.s), c.s));
   }
   if (!walk && !moe_fused(p, false)) GNOT_CK(launch_moe_combine(qin, p->P_("stage"), P * D, E, qout, P * D, c.s));
   return GNOT_OK;
@@ -1837,7 +1854,7 @@ extern "C" int gnot_forward(gnot_plan* p, const float* x, const float* theta, co
     a.X = p->P_("x"); a.ldx = p->bufs["x"].ld;
     a.Y = p->P_("scores"); a.ldy = p->bufs["scores"].ld; a.mode = CH_SOFTMAX;
     if (tr) { a.save = p->P_("gate_save"); a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D; }
-    GNOT_CK(launch_chain_fwd(a, c.s));
+    GNOT_CK(launch_chain_fwd(cw_scratch(p, a, c.s), c.s));
   }
   // query encoder (model.py:158-161)
   {
@@ -1845,7 +1862,7 @@ extern "C" int gnot_forward(gnot_plan* p, const float* x, const float* theta, co
     a.X = p->P_("xin"); a.ldx = p->bufs["xin"].ld;
     a.Y = p->P_("query0"); a.ldy = D; a.mode = CH_STORE;
     if (tr) { a.save = p->P_("x_save"); a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D; }
-    GNOT_CK(launch_chain_fwd(a, c.s));
+    GNOT_CK(launch_chain_fwd(cw_scratch(p, a, c.s), c.s));
   }
   for (int i = 0; i < p->I; ++i) {
     const std::string n = "fn" + std::to_string(i);
@@ -1860,7 +1877,7 @@ extern "C" int gnot_forward(gnot_plan* p, const float* x, const float* theta, co
     a.X = p->P_("fn" + si); a.ldx = p->bufs["fn" + si].ld;
     a.Y = p->P_("fnenc" + si); a.ldy = D; a.mode = CH_STORE;
     if (tr) { a.save = p->P_("fn_save" + si); a.save_layer_stride = p->Q[i] * D; a.save_chain_stride = NL * p->Q[i] * D; }
-    GNOT_CK(launch_chain_fwd(a, cf.s));
+    GNOT_CK(launch_chain_fwd(cw_scratch(p, a, cf.s), cf.s));
   }
   // key/value projections (model.py:67-75) and states (model.py:77-79) of every (block, input
   // function): they depend only on the input-function encodings, so all L*I of them run batched here
@@ -1893,7 +1910,7 @@ extern "C" int gnot_forward(gnot_plan* p, const float* x, const float* theta, co
     ChainArgs a = chain_args(p, p->ch_out, P);
     a.X = p->P_(p->final_query()); a.ldx = D; a.Y = out; a.ldy = p->out; a.mode = CH_STORE;
     if (tr) { a.save = p->P_("out_save"); a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D; }
-    GNOT_CK(launch_chain_fwd(a, c.s));
+    GNOT_CK(launch_chain_fwd(cw_scratch(p, a, c.s), c.s));
   }
   p->fwd_done = true;
   p->bwd_done = false;
@@ -1928,7 +1945,7 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
     if (a.b16s) { a.dz_layer_stride /= 2; a.dz_chain_stride /= 2; }   // bf16 dZ layers
     {
       ProfScope ps(cc, prof, 2.0 * a.nchains * rows * NL * (double)D * D);
-      GNOT_CK(launch_chain_bwd(a, cc.s));
+      GNOT_CK(launch_chain_bwd(cw_scratch(p, a, cc.s), cc.s));
     }
     // the weight gradients read the saved pre-activations too: a recomputed (shared) save buffer
     // must not be overwritten by the next MoE's recompute before they finish.  That guard is the
@@ -1969,7 +1986,7 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
         f.walk = walk ? 1 : 0;
         f.Y = nullptr; f.y_chain_stride = P * D;
         ProfScope ps(c, "moe_recompute", 2.0 * E * P * NL * (double)D * D);
-        GNOT_CK(launch_chain_fwd(f, c.s));
+        GNOT_CK(launch_chain_fwd(cw_scratch(p, f, c.s), c.s));
       }
       ChainArgs a = chain_args(p, m1 ? p->ch_m1[l] : p->ch_m2[l], P);
       a.dY = dquery; a.lddy = D; a.mode = CH_MOE;

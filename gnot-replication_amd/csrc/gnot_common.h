@@ -223,6 +223,10 @@ constexpr int chunk_och(int KT, int OT) {
   return c;
 }
 constexpr int chunk_f4(int KT, int OT) { return chunk_och(KT, OT) * KT * WAVE; }
+// float4 per buffer of a KT-deep weight stream: kChunkF4, or one whole output tile when that is larger
+// (KT > kChunkKB: the layer-wise kernels at d > 256)
+template <int KT>
+constexpr int pipe_buf_f4() { return KT * WAVE > kChunkF4 ? KT * WAVE : kChunkF4; }
 
 struct NoHook {
   GNOT_DEV void operator()() const {}
@@ -239,11 +243,11 @@ GNOT_DEV void mm_tiles_pipe(const float4* __restrict__ Wg, const float4* __restr
   for (int c = 0; c < NC; ++c) {
     lds_dma_wait();                                    // this chunk's DMA (issued one chunk ago) has landed
     __syncthreads();
-    float4* nb = lds + ((cnt + 1) & 1) * kChunkF4;
+    float4* nb = lds + ((cnt + 1) & 1) * pipe_buf_f4<KT>();
     if (c + 1 < NC) stage_image(nb, Wg + (c + 1) * CH4, CH4, nwaves, wave, lane);
     else if (next_W) stage_image(nb, next_W, next_f4, nwaves, wave, lane);
     if (c == 0) hook();   // e.g. prefetch the next layer's saved rows: a whole layer of MFMAs to land
-    const float4* cb = lds + (cnt & 1) * kChunkF4;
+    const float4* cb = lds + (cnt & 1) * pipe_buf_f4<KT>();
     float4 wc[OCH], wn[OCH];
 #pragma unroll
     for (int o = 0; o < OCH; ++o) wc[o] = cb[(o * KT + 0) * WAVE + lane];

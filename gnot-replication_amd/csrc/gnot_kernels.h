@@ -85,6 +85,10 @@ struct ChainArgs {
   int P;
   int nchains;         // grid.y
   const ChainLayer* layers;          // device table [nchains * nlin]
+  // d > 256 (chainw.hip, one Linear at a time): the same table in host memory and 2 * P * D floats of
+  // scratch (the activations between two Linears)
+  const ChainLayer* layers_host = nullptr;
+  float* scratch = nullptr;
   // forward
   const float* X; long ldx;          // chain input (shared by all chains)
   float* Y; long ldy; long y_chain_stride;   // output (CH_STORE/CH_SOFTMAX) or MoE stage
@@ -125,6 +129,8 @@ struct ChainArgs {
 };
 // walk or per-expert grid for a MoE call of P points (env GNOT_MOE_WALK = 0 / 1 forces, read per call)
 bool chain2_walk_choice(long P, int E);
+// d > 256: chains one Linear at a time (linear.hip + elementwise passes, chainw.hip)
+hipError_t launch_chainw(const ChainArgs& a, bool bwd, hipStream_t s);
 hipError_t launch_chain_fwd(const ChainArgs& a, hipStream_t s);
 hipError_t launch_chain_bwd(const ChainArgs& a, hipStream_t s);
 // d = 256 chains (chain2.hip): bf16x6 in both directions, output-major x6 images (pack x6 = 2) for Wp

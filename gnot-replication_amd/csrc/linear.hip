@@ -86,14 +86,14 @@ GNOT_DEV void linear_body(const LinearArgs& a, float4* wlds) {
 
 template <int D, int OC>
 __global__ void __launch_bounds__(256) linear_kernel(LinearArgs a) {
-  __shared__ __attribute__((aligned(16))) float4 wlds[2 * kChunkF4];
+  __shared__ __attribute__((aligned(16))) float4 wlds[2 * pipe_buf_f4<D / 16>()];
   linear_body<D, OC>(a, wlds);
 }
 
 // several independent projections in one launch: job = blockIdx.z (jobs live in device memory)
 template <int D, int OC>
 __global__ void __launch_bounds__(256) linear_batch_kernel(const LinearArgs* __restrict__ jobs) {
-  __shared__ __attribute__((aligned(16))) float4 wlds[2 * kChunkF4];
+  __shared__ __attribute__((aligned(16))) float4 wlds[2 * pipe_buf_f4<D / 16>()];
   const LinearArgs a = jobs[blockIdx.z];
   if ((long)blockIdx.x * 64 >= a.P) return;        // whole workgroup: no barrier is skipped unevenly
   linear_body<D, OC>(a, wlds);
@@ -135,7 +135,9 @@ int linear_oc(int D, int NO, int nsoft, int dh) {
   GNOT_LIN(128, 4) GNOT_LIN(128, 8) GNOT_LIN(144, 1) GNOT_LIN(144, 3) GNOT_LIN(144, 9) GNOT_LIN(160, 1)   \
   GNOT_LIN(160, 2) GNOT_LIN(160, 5) GNOT_LIN(160, 10) GNOT_LIN(176, 1) GNOT_LIN(176, 11) GNOT_LIN(192, 1) \
   GNOT_LIN(192, 2) GNOT_LIN(192, 3) GNOT_LIN(192, 4) GNOT_LIN(192, 6) GNOT_LIN(192, 12) GNOT_LIN(256, 1)  \
-  GNOT_LIN(256, 2) GNOT_LIN(256, 4) GNOT_LIN(256, 8)
+  GNOT_LIN(256, 2) GNOT_LIN(256, 4) GNOT_LIN(256, 8) GNOT_LIN(320, 1) GNOT_LIN(320, 2) GNOT_LIN(320, 4)   \
+  GNOT_LIN(384, 1) GNOT_LIN(384, 2) GNOT_LIN(384, 4) GNOT_LIN(448, 1) GNOT_LIN(448, 2) GNOT_LIN(448, 4)   \
+  GNOT_LIN(512, 1) GNOT_LIN(512, 2) GNOT_LIN(512, 4)
 
 hipError_t launch_linear(const LinearArgs& a, int D, hipStream_t s) {
   if (a.P <= 0) return hipSuccess;

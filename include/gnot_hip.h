@@ -32,9 +32,10 @@ typedef struct gnot_plan gnot_plan; /* opaque */
 
 /* GNOT constructor arguments, reference model.py:143 (positional order of main.py:44).
  * n_attn_hidden_dim, n_mlp_hidden_dim and n_input_hidden_dim must be equal (the reference's
- * residual adds, model.py:131/137, require it); d up to 256 (a d that is not a multiple of 16 up to 192, or 256,
- * runs on the next of those widths with exact-zero pad columns; parameters, gradients and outputs keep d);
- * d/n_head a multiple of 4 up to 64, and 16 / 32 / 64 above d = 192. */
+ * residual adds, model.py:131/137, require it); d up to 512 (a d that is not a multiple of 16 up to 192, 256,
+ * or a multiple of 64 above it runs on the next of those widths with exact-zero pad columns; parameters,
+ * gradients and outputs keep d); d/n_head a multiple of 4 up to 64, 16 / 32 / 64 in (192, 256], and a
+ * divisor of 64 above 256. */
 typedef struct gnot_config {
   int input_dim;
   int theta_dim;

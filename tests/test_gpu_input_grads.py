@@ -25,6 +25,9 @@ CASES = {
                    n_mlp_num_layers=3, n_expert=3, n_head=4, n_input_functions=2),
     "d256_I1": dict(input_dim=3, theta_dim=2, input_func_dim=3, out_dim=1, n_attn_layers=1, d=256,
                     n_mlp_num_layers=4, n_expert=2, n_head=8, n_input_functions=1),
+    # d > 256: the chains one Linear at a time (chainw.hip), padded 300 -> 320
+    "d300_I1": dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=1, d=300,
+                    n_mlp_num_layers=2, n_expert=2, n_head=75, n_input_functions=1),
 }
 
 
@@ -65,6 +68,8 @@ def _port_grads(cfg, sd64, xs, thetas, fns_per_sample, Gs):
     ("d256_I1", "fp32", "0", True),      # MoE recompute
     ("d256_I1", "bf16", "0", False),     # bf16 mode: bf16-storage MoE chains feeding the encoder backward
     ("d256_I1", "bf16", "1", False),
+    ("d300_I1", "fp32", "0", False),
+    ("d300_I1", "fp32", "0", True),
 ])
 def test_input_grads_packed_match_port(name, prec, walk, recompute, monkeypatch):
     """north_star's bar per arithmetic: 1e-4 in fp32, 1e-2 in bf16 mode."""

@@ -113,15 +113,17 @@ def test_plan_rejects_bad_config_and_batch():
 def test_padded_widths():
     """A hidden width that is not a multiple of 16 (up to 192) runs on the next multiple's kernels: the
     plan accepts it, its canonical Linears keep the model's width (the parameter shapes), and point
-    sharding refuses it; d in (192, 256) runs on the d = 256 kernels (head widths 16 / 32 / 64 there), head
-    widths must stay multiples of 4 up to 64, and d > 256 is refused."""
+    sharding refuses it; d in (192, 256) runs on the d = 256 kernels (head widths 16 / 32 / 64 there),
+    d in (256, 512] on the one-Linear-at-a-time chains (chainw.hip; head widths dividing 64), head widths
+    must stay multiples of 4 up to 64, and d > 512 is refused."""
     from gnot_amd import _lib
     lib = _lib.load()
     base = dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=1, n_mlp_num_layers=2,
                 n_expert=2, n_input_functions=1)
     plan = ctypes.c_void_p()
     for d, H, ok in ((36, 3, True), (100, 5, True), (60, 15, True), (208, 13, True), (224, 7, True),
-                     (100, 4, False), (200, 5, False), (184, 2, False), (320, 10, False)):
+                     (320, 10, True), (288, 18, True), (512, 8, True),
+                     (100, 4, False), (200, 5, False), (184, 2, False), (300, 5, False), (576, 9, False)):
         cfg = _lib.GnotConfig(**base, n_attn_hidden_dim=d, n_mlp_hidden_dim=d, n_input_hidden_dim=d, n_head=H)
         rc = lib.gnot_plan_create(ctypes.byref(cfg), ctypes.byref(plan))
         assert (rc == 0) == ok, (d, H, rc)
