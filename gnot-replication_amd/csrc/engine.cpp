@@ -1168,7 +1168,12 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
     if (tr && !p->moe_recompute) C.add(s + "m2save", E * NL * P * D, D);
     C.add(s + "query2", P * D, D);
   }
-  p->moe_walk = p->D == 256 && p->L > 0 && chain2_walk_choice(P, E);
+  // The expert grid's fused combine hands a block's stage rows to its last workgroup with write-through
+  // stores and loads, the form MI355X_MICROARCH.md validates with one workgroup per CU.  A plan that forks
+  // its weight gradients onto the side stream (below kWgradSerialPoints) can have small side-stream
+  // workgroups co-resident with the chain's, outside that form, so it takes the walk form (no hand-off,
+  // bitwise the same results, tests/test_gpu_moe_walk.py)
+  p->moe_walk = p->D == 256 && p->L > 0 && (chain2_walk_choice(P, E) || !p->serial_wgrad());
   if (!p->moe_walk) C.add("stage", E * P * D, D);
   if (D > 256) {                             // chainw.hip scratch: query-branch chains / input-function branch
     C.add("lw_scr", 2 * P * D, D);
