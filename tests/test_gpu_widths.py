@@ -45,7 +45,7 @@ CASES = {
     "d208_h13": _cfg(208, 13, 2, 1),      # dh 16, the d = 256 kernels (chain2 / linear2 / wide wgrad) padded
     "d224_h7": _cfg(224, 7, 3, 0),        # dh 32, d = 256 kernels, self-attention only
     # d > 256: the chains one Linear at a time (chainw.hip) on the fp32-MFMA projection kernel
-    "d320_h5": _cfg(320, 5, 2, 1),        # dh 64
+    "d320_h10": _cfg(320, 10, 2, 1),      # dh 32 (d * dh <= 16384: the VALU state kernel's block budget)
     "d288_h18": _cfg(288, 18, 3, 0, nl=2),  # dh 16, padded to 320, self-attention only
     "d512_h16": _cfg(512, 16, 2, 1),      # dh 32, the widest
 }

@@ -122,8 +122,9 @@ def test_padded_widths():
                 n_expert=2, n_input_functions=1)
     plan = ctypes.c_void_p()
     for d, H, ok in ((36, 3, True), (100, 5, True), (60, 15, True), (208, 13, True), (224, 7, True),
-                     (320, 10, True), (288, 18, True), (512, 8, True),
-                     (100, 4, False), (200, 5, False), (184, 2, False), (300, 5, False), (576, 9, False)):
+                     (320, 10, True), (288, 18, True), (512, 16, True), (512, 8, False),
+                     (100, 4, False), (200, 5, False), (184, 2, False), (300, 5, False), (576, 9, False),
+                     (320, 5, False)):                 # d * dh = 20480 > 16384 (attention-state blocks)
         cfg = _lib.GnotConfig(**base, n_attn_hidden_dim=d, n_mlp_hidden_dim=d, n_input_hidden_dim=d, n_head=H)
         rc = lib.gnot_plan_create(ctypes.byref(cfg), ctypes.byref(plan))
         assert (rc == 0) == ok, (d, H, rc)
