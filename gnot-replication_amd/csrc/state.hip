@@ -28,7 +28,7 @@ GNOT_DEV int find_job_s(const int* __restrict__ prefix, int njobs, int idx) {
   return lo;
 }
 
-constexpr int kMaxBlk = 4;   // 4x4 output blocks per thread: H*(dh/4)^2 <= 1024 (d <= 256, dh <= 64)
+constexpr int kMaxBlk = 4;   // 4x4 output blocks per thread: H*(dh/4)^2 = d*dh/16 <= 1024 (gnot_plan_create: d*dh <= 16384)
 // floats of one row-stage region: pts * d rounded up to whole 64-lane x 16-byte DMA instructions
 // (d > 128 takes pts = 8192 / d, e.g. 56 points x 144 = 8,064 floats: 31.5 instructions)
 __host__ __device__ constexpr int state_stage_floats(int pts, int d) { return (pts * d + 255) / 256 * 256; }
