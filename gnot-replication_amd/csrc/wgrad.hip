@@ -380,13 +380,6 @@ constexpr int kWRawSlot = 2 * 2 * 64;            // u32x4 per wave-private raw s
 constexpr int kWRawSlots = 2;
 // LDS: two fragment buffers | 8 waves x 2 raw slots (96 + 64 = 160 KiB at NP = 3)
 constexpr size_t w_lds_bytes(int np) { return (2 * (size_t)w_buf(np) + 8 * kWRawSlots * kWRawSlot) * 16; }
-#ifndef GNOT_X6W_PF
-#define GNOT_X6W_PF 0
-#endif
-// L2 prefetch distance of the raw rows (stages ahead of the one being multiplied; 0 = none): one dword
-// load per thread per stage touches every 64-byte half-line of the stage's dZ (waves 0-3) and X rows
-// (waves 4-7), so the LDS-DMA of that stage, issued GNOT_X6W_PF - 3 iterations later, reads L2
-constexpr int kWPf = GNOT_X6W_PF;
 
 GNOT_DEV void x6_mfma6(const u32x4 (&a)[3], const u32x4 (&b)[3], f32x16& c) {
 #define GNOT_MFMA32(X, Y) \
@@ -469,33 +462,6 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
     }
   };
   const unsigned raw_addr = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) u32x4*)raw + 4u * lane;
-  // L2 prefetch (kWPf): a plain descriptor (the asm load needs SGPR words) of this wave's operand; the
-  // loaded dword is never read -- `pf` only keeps its register reserved while loads are in flight, and
-  // the counted waits below leave the younger prefetch in flight (vmcnt counts it in issue order)
-  typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
-  float pf = 0.f;
-  u32x4v pdesc{};
-  unsigned pvoff = 0, pld = 0;
-  if constexpr (kWPf > 0) {
-    const bool pb_op = (wave >> 2) != 0;
-    const unsigned long long pa = reinterpret_cast<unsigned long long>(pb_op ? J.x + pb * J.ldx : J.dz + pb * J.lddz);
-    pld = (unsigned)(pb_op ? J.ldx : J.lddz) * 4u;
-    pdesc = u32x4v{(unsigned)__builtin_amdgcn_readfirstlane((unsigned)pa),
-                   (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(pa >> 32)) & 0xffffu,
-                   (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(nsp * (long)pld)), 0x00020000u};
-    pvoff = (unsigned)((tid & 255) >> 4) * pld + (unsigned)(tid & 15) * 64u;
-  }
-  auto prefetch = [&](int st) __attribute__((always_inline)) {
-    if constexpr (kWPf > 0) {
-      const unsigned off = pvoff + (unsigned)(st * kWStage) * pld;
-      asm volatile("buffer_load_dword %0, %1, %2, 0 offen" : "+v"(pf) : "v"(off), "s"(pdesc) : "memory");
-    }
-  };
-  // counted wait for stage s + 1's rows: younger are stage s + 2's four DMAs and (kWPf) one prefetch
-  auto wait_rows = [&]() __attribute__((always_inline)) {
-    if constexpr (kWPf > 0) c2_wait_vm<5>();
-    else c2_wait_vm<4>();
-  };
   // this thread's 8 points of stage st (its slot's DMAs retired by the caller's counted wait)
   auto raw_read = [&](int st) __attribute__((always_inline)) {
     const unsigned a = raw_addr + (unsigned)((st & 1) * kWRawSlot * 16);
@@ -566,15 +532,10 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
   // take the plain double-buffered loop)
   if (nst > 0) {
     // prologue: stages 0 and 1 requested; stage 0 read (its slot then refilled with stage 2) and staged
-    if constexpr (kWPf > 0) {
-#pragma unroll
-      for (int k = 3; k < kWPf - 1; ++k) prefetch(k);    // oldest: retired by any later wait, counts unchanged
-    }
     raw_dma(0);
     raw_dma(1);
     c2_wait_vm<4>();
     raw_read(0);
-    prefetch(kWPf - 1);
     raw_dma(2);
     stage(0);
     lds_barrier();
@@ -635,9 +596,8 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
     // slot refilled with stage s + 3, and staged while stage s is multiplied
     auto run = [&](auto GEL, auto MASK) {
       for (int s = 0; s + 1 < nst; ++s) {
-        wait_rows();
+        c2_wait_vm<4>();
         raw_read(s + 1);
-        prefetch(s + kWPf);
         raw_dma(s + 3);
         fused(buf, GEL, MASK);
         lds_barrier();
@@ -654,9 +614,8 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
       }
     } else {
       for (int s = 0; s + 1 < nst; ++s) {
-        wait_rows();
+        c2_wait_vm<4>();
         raw_read(s + 1);
-        prefetch(s + kWPf);
         raw_dma(s + 3);
         compute(buf);
         stage(buf ^ 1);
@@ -666,7 +625,7 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
     }
     compute(buf);   // the last stage
     // the DMAs of the two stages past the end (zeros) land before the workgroup's LDS is released
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(pf) :: "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
 
   // partials -> slab [split][128-tile][128 x (128 + 1)] (the pgemm_kernel layout)
