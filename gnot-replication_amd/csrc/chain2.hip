@@ -532,6 +532,9 @@ __global__ void __launch_bounds__(64 * kC2Waves, 2) chain2_fwd_kernel(ChainArgs 
     for (int T = 0; T < OTL; ++T)
 #pragma unroll
       for (int r = 0; r < 4; ++r) y[T][r] *= s;
+    // B16: the stage term as the fused combine's bf16 stage rows hold it (the fp32 stage of the combine
+    // pass then sums the same values: every soft-MoE form bitwise equal)
+    if constexpr (B16) round_rows_bf16<OTL>(y);
   }
   if constexpr (OTL == 16) {
     if (a.combine != nullptr) {               // fused combine: write-through stage rows (D = 256)
@@ -855,6 +858,7 @@ __global__ void __launch_bounds__(64 * kC2Waves, 2) chain2_bwd_kernel(ChainArgs 
       if constexpr (B16) store_rows_b16_sc1<KT0>(dx, make_rsrc(a.dX + e * a.dx_chain_stride + rbase, lay_b16), rowb, lane);
       else store_rows_sc1<KT0>(dx, make_rsrc(a.dX + e * a.dx_chain_stride + row0 * D, lay_bytes), voff);
     } else {
+      if constexpr (B16) round_rows_bf16<KT0>(dx);   // the fused combine's bf16 stage value (see the forward)
       store_rows<KT0>(dx, a.dX + e * a.dx_chain_stride, a.lddx, p, valid, a.in_dim, lane);
     }
   }
@@ -897,12 +901,11 @@ static hipError_t launch_chain2_d(const ChainArgs& a, bool bwd, hipStream_t s) {
     }                                                                                                    \
   } while (0)
   if (a.b16s) {
-    // bf16 storage: soft-MoE experts (d x d chains) in bf16 mode.  The expert terms are bf16 (the stage
-    // rows, or the walk form's rounding), so the expert grid sums them with the fused combine only;
-    // a forward without saves (inference, MoE recompute's first pass) rounds its terms alike
+    // bf16 storage: soft-MoE experts (d x d chains) in bf16 mode.  The expert terms are bf16 in every
+    // form (the fused combine's stage rows; the walk form's and the fp32 stage's rounding), so the expert
+    // grid with the fused combine, the grid with the combine pass and the walk form give the same bits
     if constexpr (NP == 1) {
       if (a.mode != CH_MOE || a.KT0 != DT || a.OTL != DT) return hipErrorInvalidValue;
-      if (!a.walk && !a.combine && (bwd || a.Y)) return hipErrorInvalidValue;
 #define GNOT_C2_B16(W_)                                                                                  \
   if (bwd) {                                                                                             \
     GNOT_C2_ATTR((chain2_bwd_kernel<D, DT, DT, 1, W_, true>));                                           \

@@ -1172,12 +1172,7 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
     if (tr && !p->moe_recompute) C.add(s + "m2save", E * NL * P * D, D);
     C.add(s + "query2", P * D, D);
   }
-  // The expert grid's fused combine hands a block's stage rows to its last workgroup with write-through
-  // stores and loads, the form MI355X_MICROARCH.md validates with one workgroup per CU.  A plan that forks
-  // its weight gradients onto the side stream (below kWgradSerialPoints) can have small side-stream
-  // workgroups co-resident with the chain's, outside that form, so it takes the walk form (no hand-off,
-  // bitwise the same results, tests/test_gpu_moe_walk.py)
-  p->moe_walk = p->D == 256 && p->L > 0 && (chain2_walk_choice(P, E) || !p->serial_wgrad());
+  p->moe_walk = p->D == 256 && p->L > 0 && chain2_walk_choice(P, E);
   if (!p->moe_walk) C.add("stage", E * P * D, D);
   if (D > 256) {                             // chainw.hip scratch: query-branch chains / input-function branch
     C.add("lw_scr", 2 * P * D, D);
@@ -1799,7 +1794,15 @@ int attn_backward(Ctx& c, int l, bool cross) {
 // (262,144 points, E = 8; profiles/r04_chain_grid.txt): bf16x6 forward 6.76 ms + 0.47 pass against 7.51
 // fused, backward 8.27 + 0.47 against 8.73; bf16 storage forward 4.01 + 0.47 against 4.08 fused
 static bool moe_walk(gnot_plan* p) { return p->moe_walk; }
-static bool moe_fused(gnot_plan* p, bool bwd) { return p->D == 256 && !p->moe_walk && (bwd || p->b16s()); }
+// The expert grid's fused combine hands a block's stage rows to its last workgroup with write-through
+// stores and loads, the form MI355X_MICROARCH.md validates with one workgroup per CU.  A plan that forks
+// its weight gradients onto the side stream (below kWgradSerialPoints) can have small side-stream
+// workgroups co-resident with the chain's, outside that form, so it sums the stage with the combine pass
+// (no hand-off; bitwise the same results, tests/test_gpu_recompute.py).  The walk form, its round-4
+// choice for those plans, made configs[0] 15 % slower (9.6 -> 11.0 ms per step).
+static bool moe_fused(gnot_plan* p, bool bwd) {
+  return p->D == 256 && !p->moe_walk && p->serial_wgrad() && (bwd || p->b16s());
+}
 // save (and dZ) layout of a soft-MoE chain call: fp32 [NL][P][D] per expert, or in bf16 mode 2 NL bf16
 // layers per expert (ChainArgs::b16s)
 static void moe_save_strides(gnot_plan* p, ChainArgs& a) {
