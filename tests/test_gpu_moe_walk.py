@@ -16,8 +16,8 @@ pytestmark = pytest.mark.gpu
 def _run(monkeypatch, walk, recompute, E, I, d=256, prec="fp32"):
     from gnot_amd import GNOT
     monkeypatch.setenv("GNOT_MOE_WALK", walk)
-    # serial weight gradients: a small plan that forks them takes the walk form (engine.cpp), and the
-    # grid run here must be the expert grid with its fused combine
+    # serial weight gradients: a small plan that forks them sums the expert grid's stage with the combine
+    # pass (engine.cpp moe_fused), and the grid run here must be the grid with its fused combine
     monkeypatch.setenv("GNOT_WGRAD_OVERLAP", "0")
     dev = torch.device("cuda")
     torch.manual_seed(17)
