@@ -52,13 +52,16 @@ def pmc_traffic(workload, kind, launches_per_step):
     (profiles/pmc_traffic.json, written by scripts/pmc_traffic.py: FETCH_SIZE x 2 for the gfx950 half-count
     of wide streaming reads + WRITE_SIZE, MI355X_MICROARCH.md HBM section, summed over ALL of the class's
     dispatches of a step and divided by their count -- the same per-launch mean as `achieved`).  None
-    when no entry exists or the entry's launches per step differ from this run's (another tree)."""
+    when no entry exists, or the entry was measured on other kernels: its source hash (gnot_amd._lib.
+    source_hash over the library's sources) differs from this tree's, or its launches per step differ."""
+    from gnot_amd import _lib
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         e = json.load(open(path))[f"{workload}/{kind}"]
     except (OSError, KeyError, ValueError):
         return None
-    if e.get("launches_per_step") != launches_per_step:
+    sh = _lib.source_hash()
+    if sh is None or e.get("source_hash") != sh or e.get("launches_per_step") != launches_per_step:
         return None
     return e["bytes_per_launch"]
 

@@ -119,12 +119,20 @@ GNOT_DEV void round_rows_bf16(float (&a)[KT][4]) {
 }
 
 // The fused soft-MoE combine (model.py:128-131 / 134-137): called by every workgroup of the expert grid
-// after its write-through stage stores.  Hand-off (MI355X_MICROARCH.md, "Valid forms", first table row):
-// every wave waits for its own stores (vmcnt(0)), a barrier, then ONE lane adds to the block's counter
-// (agent scope) for the whole workgroup; the workgroup whose add returns E - 1 is the last, resets the
-// counter for the next launch and, after a barrier, sums the block's E stage rows with sc1 loads, in
-// expert order, onto `base` (or 0): bitwise the separate combine pass it replaces.  One workgroup per CU
-// (the chain kernels' LDS), as that hand-off form requires.
+// after its write-through stage stores.  Hand-off (MI355X_MICROARCH.md, "Valid forms", producer with sc1
+// stores, consumer "always" form): every wave waits for its own stores (vmcnt(0)), a barrier, then ONE
+// lane adds to the block's counter (agent scope) for the whole workgroup; the workgroup whose add returns
+// E - 1 is the last: that lane resets the counter for the next launch, runs ONE agent-scope acquire
+// (buffer_inv sc1) and waits for it before the barrier its siblings join, then the workgroup sums the
+// block's E stage rows with sc1 loads, in expert order, onto `base` (or 0): bitwise the separate combine
+// pass it replaces.
+// Round 4 had no acquire: sc1 stores + sc1 loads alone are valid only with ONE workgroup per CU (the
+// guide's measured table, row 1).  That held for the chain grid alone, but not when other kernels share
+// the CUs: the side-stream weight gradients of a small plan, the comm stream's RCCL kernels at N > 1, the
+// input-function branch on side2, or a second process on the same GPU (the 2-rank sharded 70k test of
+// r04sf, whose block-0 cross-attention gradients -- downstream of the ffn1 combine's dX sum -- came out
+// wrong once).  With the acquire the form holds at any occupancy; it costs one L1 invalidate per 128-point
+// block (the last workgroup only, ~2 us while the other 7 experts' workgroups of the CU wave keep running).
 // B16 (bf16 mode, bf16 storage): the stage rows are RNE bf16 pair-interleaved rows (512 B per point), summed
 // in fp32 in the same order (the walk form rounds each expert's term the same way)
 template <bool B16>
@@ -136,7 +144,11 @@ GNOT_DEV void moe_combine_last(const float* stage, long stage_stride, int E, con
   if (threadIdx.x == 0) {
     const int old = __hip_atomic_fetch_add(counters + blk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last = old == E - 1;
-    if (old == E - 1) __hip_atomic_store(counters + blk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == E - 1) {
+      __hip_atomic_store(counters + blk, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   }
   __syncthreads();
   if (!last) return;

@@ -5,6 +5,7 @@ INTEGRATION.md): plain pointers and sizes, one `gnot_plan` per model.  There is 
 fallback: if the shared library is missing or cannot be loaded, importing the product path fails.
 """
 import ctypes
+import hashlib
 import os
 import subprocess
 
@@ -49,6 +50,27 @@ def build(jobs=8, quiet=True):
     if res.returncode != 0:
         raise RuntimeError("building libgnot_hip.so failed:\n" + (res.stdout or "") + (res.stderr or ""))
     return LIB_PATH
+
+
+# every file the library's code depends on (csrc/Makefile's SRCS, its headers and its flags)
+SOURCES = ["Makefile", "gnot_common.h", "gnot_kernels.h", "x6_core.h", "pack.hip", "linear.hip", "linear2.hip",
+           "chain.hip", "chain2.hip", "chainw.hip", "wgrad.hip", "state.hip", "attn.hip", "attn_mfma.hip", "misc.hip",
+           "train.hip", "engine.cpp"]
+
+
+def source_hash():
+    """16 hex digits of sha256 over the library's sources (SOURCES + include/gnot_hip.h): the identity of
+    the kernels a measurement was taken on.  profiles/pmc_traffic.json stores it per entry, and bench.py
+    reports an entry's traffic only for the same hash (a changed kernel or launch sequence prints null).
+    None when an experiment build is loaded instead (GNOT_LIB)."""
+    if os.environ.get("GNOT_LIB"):
+        return None
+    h = hashlib.sha256()
+    for f in [os.path.join(CSRC, n) for n in SOURCES] + [os.path.join(os.path.dirname(PKG_ROOT), "include", "gnot_hip.h")]:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def _declare(lib):

@@ -24,6 +24,8 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gnot-replication_amd"))
+from gnot_amd._lib import source_hash  # noqa: E402
 
 
 def dispatches(d, counter):
@@ -64,7 +66,7 @@ def main():
     out_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     table = json.load(open(out_path)) if os.path.exists(out_path) else {}
     table[key] = {"kernels": [sub] + ([follow] if follow else []), "launches": launches,
-                  "launches_per_step": int(per_step),
+                  "launches_per_step": int(per_step), "source_hash": source_hash(),
                   "fetch_size_kb_per_launch": fetch_kb / launches, "write_size_kb_per_launch": write_kb / launches,
                   "bytes_per_launch": int((2 * fetch_kb + write_kb) * 1024 / launches),
                   "source": f"{os.path.basename(fdir)}, {os.path.basename(wdir)} (sum over dispatches / launches)"}

@@ -6,8 +6,16 @@ parameter gradients are summed over the ranks.  Summed group by group inside the
 collective per weight-gradient group, issued as soon as the group is written), the gradients must be
 BITWISE those of the plain path -- the backward alone, then one all-reduce of the flat gradient buffer
 (two ranks: every element is the same a + b).  d = 64 (chain.hip, the 128-tile weight gradients) and
-d = 256 with 8 experts (chain2.hip, the wide kernels and the fused soft-MoE combine), fp32 and bf16
-mode.  The reference is single-device (main.py:27); SURVEY.md section 5 asks for the overlap.
+d = 256 with 8 experts (chain2.hip, the wide weight-gradient kernels), fp32 and bf16 mode.
+
+The plans have ~1.5k points, below the size from which the engine runs its weight gradients serially
+(kWgradSerialPoints), so by default they fork the weight gradients onto the side stream and sum the soft-MoE
+experts with the moe_combine pass.  GNOT_WGRAD_OVERLAP=0 forces the serial form: each group's collective
+is then issued on the comm stream right behind the caller's stream, and at d = 256 the expert grid sums
+its experts with the FUSED combine (inter-workgroup hand-off, chain2.hip moe_combine_last) while the
+collectives of earlier groups and the other rank's kernels run beside it -- the setting of every N > 1
+bench run of configs[2]/[3].  Both forms must give the flat all-reduce's bits.
+The reference is single-device (main.py:27); SURVEY.md section 5 asks for the overlap.
 """
 import os
 import socket
@@ -31,9 +39,9 @@ def _free_port():
     return port
 
 
-def _rank(rank, world, port, d, E, prec, q):
+def _rank(rank, world, port, d, E, prec, overlap, q):
     sys.path[:0] = [ROOT, os.path.join(ROOT, "gnot-replication_amd"), os.path.join(ROOT, "tests")]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GNOT_WGRAD_OVERLAP=overlap)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from gnot_amd import GNOT
@@ -70,13 +78,14 @@ def _rank(rank, world, port, d, E, prec, q):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("overlap", ["1", "0"])
 @pytest.mark.parametrize("d,E,prec", [(64, 3, "fp32"), (256, 8, "fp32"), (256, 8, "bf16")])
-def test_overlapped_grad_allreduce_equals_flat_allreduce(d, E, prec):
+def test_overlapped_grad_allreduce_equals_flat_allreduce(d, E, prec, overlap):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, world, port, d, E, prec, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank, args=(r, world, port, d, E, prec, overlap, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=200) for _ in range(world))

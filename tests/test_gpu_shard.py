@@ -144,14 +144,20 @@ def test_point_sharded_gnot_rccl_path():
 
 
 @pytest.mark.timeout(600)
-def test_point_sharded_configs3_widths_70k_points(mid_case):
+@pytest.mark.parametrize("overlap", ["auto", "0"])
+def test_point_sharded_configs3_widths_70k_points(mid_case, overlap):
     """configs[3]'s model widths (d=256, 8 heads, 8 experts, 4-layer MLPs, one 805-point input function;
     L = 1 block) on one 70,000-point mesh split over 2 ranks (35,000 points each, gloo host staging on one
     GPU) vs the float64 oracle at 1e-4: the sharded run takes the kernels a 1M / 8 rank does -- the MFMA
     attention apply / K-V backward (>= 8,192 points), the MFMA state partials (GNOT_STATE_MFMA_MIN=16384
     in the ranks: per-rank groups of 35,000 points), the wide weight gradients -- and real exchange
     tables (the scramble of 8 heads over 70,000 points is 16 runs per rank pair).  Anchor: the all-point
-    state sums model.py:98-100 (all-reduced) and the head-major reshape model.py:103-104 (all-to-all)."""
+    state sums model.py:98-100 (all-reduced) and the head-major reshape model.py:103-104 (all-to-all).
+    overlap "auto": 35,000 points per rank fork their weight gradients onto the side stream and sum the
+    soft-MoE experts with the moe_combine pass; "0" (GNOT_WGRAD_OVERLAP=0) runs them serially, so the expert
+    grid sums its experts with the fused combine's inter-workgroup hand-off (chain2.hip moe_combine_last)
+    while the other rank's process and side2's input-function branch share the GPU -- the setting in which
+    round 4 saw wrong block-0 cross-attention gradients once."""
     fx, G = mid_case
     fx = dict(fx, G=G)
     world = 2
@@ -159,6 +165,8 @@ def test_point_sharded_configs3_widths_70k_points(mid_case):
     q = ctx.Queue()
     port = _free_port()
     env = {"GNOT_STATE_MFMA_MIN": "16384"}
+    if overlap != "auto":
+        env["GNOT_WGRAD_OVERLAP"] = overlap
     procs = [ctx.Process(target=_rank, args=(r, world, port, fx["cfg"], [int(fx["x_off"][-1])], [[805]], q),
                          kwargs=dict(fx=fx, env=env))
              for r in range(world)]
