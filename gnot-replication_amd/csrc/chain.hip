@@ -12,6 +12,8 @@
 //              (model.py:128-130; the residual add + sum over experts is moe_combine / the consumer)
 // The backward kernel walks the same chain in reverse with the transposed weight images,
 // re-applying GELU'(saved pre-activation), and writes each layer's dZ for the weight-gradient pass.
+#include <type_traits>
+
 #include "gnot_common.h"
 #include "gnot_kernels.h"
 
@@ -23,8 +25,10 @@ namespace gnot {
 constexpr int kChainWaves = 4;
 
 // 3 waves per SIMD (<= 168 VGPRs + AGPRs) at d <= 128: a 10k-point MoE launch (2,500 waves) is then
-// ONE round on the 1,024 SIMDs instead of a full round plus a 20 % tail round at 2 waves per SIMD
-template <int D, int KT0, int OTL>
+// ONE round on the 1,024 SIMDs instead of a full round plus a 20 % tail round at 2 waves per SIMD.
+// NP: operand pieces, 3 = bf16x6 (fp32-exact, k-major x6 images, pack x6 = 1), 1 = the bf16 arithmetic
+// mode (one RNE bf16 piece, pack x6 = 4)
+template <int D, int KT0, int OTL, int NP>
 __global__ void __launch_bounds__(64 * kChainWaves) __attribute__((amdgpu_waves_per_eu(D <= 128 ? 3 : 1)))
 chain_fwd_kernel(ChainArgs a) {
   constexpr int DT = D / 16;
@@ -39,8 +43,8 @@ chain_fwd_kernel(ChainArgs a) {
   __shared__ __attribute__((aligned(16))) float4 wlds[2 * x6_buf_f4(D)];
   int cnt = 0;
   // the weight stream: layer 0 | hidden layers | last layer, one chunk always in flight
-  stage_image(wlds, L[0].Wp, x6_chunk_f4<D>(KT0, DT), kChainWaves, wave, lane);
-  auto next_f4 = [&](int l) { return (l == nl - 1) ? x6_chunk_f4<D>(DT, OTL) : x6_chunk_f4<D>(DT, DT); };
+  stage_image(wlds, L[0].Wp, x6_chunk_f4<D, NP>(KT0, DT), kChainWaves, wave, lane);
+  auto next_f4 = [&](int l) { return (l == nl - 1) ? x6_chunk_f4<D, NP>(DT, OTL) : x6_chunk_f4<D, NP>(DT, DT); };
 
   float h[DT][4];
   {
@@ -48,7 +52,7 @@ chain_fwd_kernel(ChainArgs a) {
     load_rows<KT0>(x0, a.X, a.ldx, p, valid, a.in_dim, lane);
     f32x4 acc[DT];
     init_bias<DT>(acc, L[0].bias, lane);
-    mm_tiles_pipe_x6<D, KT0, DT>(L[0].Wp, L[1].Wp, next_f4(1), wlds, cnt, x0, acc, kChainWaves, wave, lane);
+    mm_tiles_pipe_x6<D, KT0, DT, NP>(L[0].Wp, L[1].Wp, next_f4(1), wlds, cnt, x0, acc, kChainWaves, wave, lane);
     acc_to_regs<DT>(acc, h);
   }
   if (save) store_rows<DT>(h, save, D, p, valid, D, lane);
@@ -60,7 +64,8 @@ chain_fwd_kernel(ChainArgs a) {
   for (int l = 1; l < nl - 1; ++l) {
     f32x4 acc[DT];
     init_bias<DT>(acc, L[l].bias, lane);
-    mm_tiles_pipe_x6<D, DT, DT>(L[l].Wp, L[l + 1].Wp, next_f4(l + 1), wlds, cnt, h, acc, kChainWaves, wave, lane);
+    mm_tiles_pipe_x6<D, DT, DT, NP>(L[l].Wp, L[l + 1].Wp, next_f4(l + 1), wlds, cnt, h, acc, kChainWaves, wave,
+                                    lane);
     acc_to_regs<DT>(acc, h);
     if (save) store_rows<DT>(h, save + l * a.save_layer_stride, D, p, valid, D, lane);
 #pragma unroll
@@ -73,7 +78,7 @@ chain_fwd_kernel(ChainArgs a) {
   {
     f32x4 acc[OTL];
     init_bias<OTL>(acc, L[nl - 1].bias, lane);
-    mm_tiles_pipe_x6<D, DT, OTL>(L[nl - 1].Wp, nullptr, 0, wlds, cnt, h, acc, kChainWaves, wave, lane);
+    mm_tiles_pipe_x6<D, DT, OTL, NP>(L[nl - 1].Wp, nullptr, 0, wlds, cnt, h, acc, kChainWaves, wave, lane);
     acc_to_regs<OTL>(acc, y);
   }
   if (save) store_rows<OTL>(y, save + (nl - 1) * a.save_layer_stride, D, p, valid, 16 * OTL, lane);
@@ -119,7 +124,9 @@ chain_fwd_kernel(ChainArgs a) {
   }
 }
 
-template <int D, int KT0, int OTL>
+// NP = 3: exact fp32 MFMA on fp32 fragment images of W^T; NP = 1 (bf16 mode): one RNE bf16 piece per
+// operand on k-major one-piece images of W^T (pack x6 = 4), fp32 accumulation
+template <int D, int KT0, int OTL, int NP>
 __global__ void __launch_bounds__(64 * kChainWaves) chain_bwd_kernel(ChainArgs a) {
   constexpr int DT = D / 16;
   const int lane = threadIdx.x & 63;
@@ -132,15 +139,28 @@ __global__ void __launch_bounds__(64 * kChainWaves) chain_bwd_kernel(ChainArgs a
   const ChainLayer* L = a.layers + e * nl;
   const float* save = a.save + e * a.save_chain_stride;
   float* dz = a.dz ? a.dz + e * a.dz_chain_stride : nullptr;
-  __shared__ __attribute__((aligned(16))) float4 wlds[2 * kChunkF4];
+  constexpr bool B1 = NP == 1;
+  __shared__ __attribute__((aligned(16))) float4 wlds[B1 ? 2 * x6_buf_f4(D) : 2 * kChunkF4];
   int cnt = 0;
+  // chunk of a KT-deep, OT-wide transposed image: fp32 fragment tiles, or one-piece k-major blocks
+  auto cf4 = [](int KT, int OT) { return B1 ? x6_chunk_f4<D, 1>(KT, OT) : chunk_f4(KT, OT); };
+  // acc += W^T in over the KT-deep image Wg (the weight stream of the pipe of this arithmetic)
+  auto mm = [&](auto KTc, auto OTc, const float4* Wg, const float4* nW, int nf4, const float (&in)[decltype(KTc)::value][4],
+                f32x4 (&acc)[decltype(OTc)::value], auto hook) __attribute__((always_inline)) {
+    constexpr int KT = decltype(KTc)::value, OT = decltype(OTc)::value;
+    if constexpr (B1) mm_tiles_pipe_x6<D, KT, OT, 1>(Wg, nW, nf4, wlds, cnt, in, acc, kChainWaves, wave, lane, hook);
+    else mm_tiles_pipe<KT, OT>(Wg, nW, nf4, wlds, cnt, in, acc, kChainWaves, wave, lane, hook);
+  };
+  using IOTL = std::integral_constant<int, OTL>;
+  using IDT = std::integral_constant<int, DT>;
+  using IKT0 = std::integral_constant<int, KT0>;
   // transposed-weight stream in reverse layer order: last | hidden (nl-2 .. 1) | first (if dX)
-  stage_image(wlds, L[nl - 1].WpT, chunk_f4(OTL, DT), kChainWaves, wave, lane);
+  stage_image(wlds, L[nl - 1].WpT, cf4(OTL, DT), kChainWaves, wave, lane);
   auto next_W = [&](int l) -> const float4* {      // the layer processed after layer l
     if (l - 1 >= 1) return L[l - 1].WpT;
     return a.dX ? L[0].WpT : nullptr;
   };
-  auto next_f4 = [&](int l) { return (l - 1 >= 1) ? chunk_f4(DT, DT) : chunk_f4(DT, KT0); };
+  auto next_f4 = [&](int l) { return (l - 1 >= 1) ? cf4(DT, DT) : cf4(DT, KT0); };
 
   // ---- gradient at the chain output
   float dy[OTL][4];
@@ -190,8 +210,7 @@ __global__ void __launch_bounds__(64 * kChainWaves) chain_bwd_kernel(ChainArgs a
     f32x4 acc[DT];
     init_bias<DT>(acc, nullptr, lane);
     auto pre = [&]() { load_rows<DT>(hs, save + (nl - 2) * a.save_layer_stride, D, p, valid, D, lane); };
-    mm_tiles_pipe<OTL, DT>(L[nl - 1].WpT, next_W(nl - 1), next_f4(nl - 1), wlds, cnt, dy, acc, kChainWaves, wave, lane,
-                           pre);
+    mm(IOTL{}, IDT{}, L[nl - 1].WpT, next_W(nl - 1), next_f4(nl - 1), dy, acc, pre);
     acc_to_regs<DT>(acc, gr);
   }
   // ---- hidden Linears, reverse
@@ -204,7 +223,7 @@ __global__ void __launch_bounds__(64 * kChainWaves) chain_bwd_kernel(ChainArgs a
     f32x4 acc[DT];
     init_bias<DT>(acc, nullptr, lane);
     auto pre = [&]() { load_rows<DT>(hs, save + (l - 1) * a.save_layer_stride, D, p, valid, D, lane); };
-    mm_tiles_pipe<DT, DT>(L[l].WpT, next_W(l), next_f4(l), wlds, cnt, gr, acc, kChainWaves, wave, lane, pre);
+    mm(IDT{}, IDT{}, L[l].WpT, next_W(l), next_f4(l), gr, acc, pre);
     acc_to_regs<DT>(acc, gr);
   }
   // ---- first Linear (hs now holds the saved pre-activation of Linear 0)
@@ -216,21 +235,21 @@ __global__ void __launch_bounds__(64 * kChainWaves) chain_bwd_kernel(ChainArgs a
   if (a.dX) {
     f32x4 acc[KT0];
     init_bias<KT0>(acc, nullptr, lane);
-    mm_tiles_pipe<DT, KT0>(L[0].WpT, nullptr, 0, wlds, cnt, gr, acc, kChainWaves, wave, lane);
+    mm(IDT{}, IKT0{}, L[0].WpT, nullptr, 0, gr, acc, NoHook());
     float dx[KT0][4];
     acc_to_regs<KT0>(acc, dx);
     store_rows<KT0>(dx, a.dX + e * a.dx_chain_stride, a.lddx, p, valid, a.in_dim, lane);
   }
 }
 
-template <int D>
-static hipError_t launch_chain_d(const ChainArgs& a, bool bwd, hipStream_t s) {
+template <int D, int NP>
+static hipError_t launch_chain_np(const ChainArgs& a, bool bwd, hipStream_t s) {
   constexpr int DT = D / 16;
   const dim3 grid((a.P + 16 * kChainWaves - 1) / (16 * kChainWaves), a.nchains), block(64 * kChainWaves);
 #define GNOT_CHAIN_CASE(K0, OL)                                                              \
   if (a.KT0 == K0 && a.OTL == OL) {                                                           \
-    if (bwd) hipLaunchKernelGGL((chain_bwd_kernel<D, K0, OL>), grid, block, 0, s, a);          \
-    else hipLaunchKernelGGL((chain_fwd_kernel<D, K0, OL>), grid, block, 0, s, a);              \
+    if (bwd) hipLaunchKernelGGL((chain_bwd_kernel<D, K0, OL, NP>), grid, block, 0, s, a);      \
+    else hipLaunchKernelGGL((chain_fwd_kernel<D, K0, OL, NP>), grid, block, 0, s, a);          \
     return hipGetLastError();                                                                 \
   }
   GNOT_CHAIN_CASE(1, 1)
@@ -239,6 +258,10 @@ static hipError_t launch_chain_d(const ChainArgs& a, bool bwd, hipStream_t s) {
   GNOT_CHAIN_CASE(DT, DT)
 #undef GNOT_CHAIN_CASE
   return hipErrorInvalidValue;
+}
+template <int D>
+static hipError_t launch_chain_d(const ChainArgs& a, bool bwd, hipStream_t s) {
+  return a.np == 1 ? launch_chain_np<D, 1>(a, bwd, s) : launch_chain_np<D, 3>(a, bwd, s);
 }
 
 static hipError_t launch_chain(const ChainArgs& a, bool bwd, hipStream_t s) {

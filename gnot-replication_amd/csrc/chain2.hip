@@ -118,23 +118,19 @@ GNOT_DEV void round_rows_bf16(float (&a)[KT][4]) {
     for (int r = 0; r < 4; ++r) a[T][r] = bf16_lo(pk_bf16(a[T][r], 0.f));
 }
 
-// The fused soft-MoE combine (model.py:128-131 / 134-137): called by every workgroup of the expert grid
-// after its write-through stage stores.  Hand-off (MI355X_MICROARCH.md, "Valid forms", producer with sc1
-// stores, consumer "always" form): every wave waits for its own stores (vmcnt(0)), a barrier, then ONE
-// lane adds to the block's counter (agent scope) for the whole workgroup; the workgroup whose add returns
-// E - 1 is the last: that lane resets the counter for the next launch, runs ONE agent-scope acquire
-// (buffer_inv sc1) and waits for it before the barrier its siblings join, then the workgroup sums the
-// block's E stage rows with sc1 loads, in expert order, onto `base` (or 0): bitwise the separate combine
-// pass it replaces.
-// Round 4 had no acquire: sc1 stores + sc1 loads alone are valid only with ONE workgroup per CU (the
-// guide's measured table, row 1).  That held for the chain grid alone, but not when other kernels share
-// the CUs: the side-stream weight gradients of a small plan, the comm stream's RCCL kernels at N > 1, the
-// input-function branch on side2, or a second process on the same GPU (the 2-rank sharded 70k test of
-// r04sf, whose block-0 cross-attention gradients -- downstream of the ffn1 combine's dX sum -- came out
-// wrong once).  With the acquire the form holds at any occupancy; it costs one L1 invalidate per 128-point
-// block (the last workgroup only, ~2 us while the other 7 experts' workgroups of the CU wave keep running).
-// B16 (bf16 mode, bf16 storage): the stage rows are RNE bf16 pair-interleaved rows (512 B per point), summed
-// in fp32 in the same order (the walk form rounds each expert's term the same way)
+// The fused soft-MoE combine (model.py:128-131 / 134-137), OPT-IN (GNOT_MOE_FUSED=1, engine.cpp moe_fused):
+// called by every workgroup of the expert grid after its write-through (sc1) stage stores.  Every wave waits
+// for its own stores (vmcnt(0)), a barrier, then ONE lane runs an agent-scope release and adds to the block's
+// counter (agent scope) for the whole workgroup; the workgroup whose add returns E - 1 is the last: that lane
+// resets the counter for the next launch, runs ONE agent-scope acquire and waits for it before the barrier
+// its siblings join, then the workgroup sums the block's E stage rows with sc1 loads, in expert order, onto
+// `base` (or 0): bitwise the separate combine pass.  This is MI355X_MICROARCH.md's general form, valid
+// whatever else shares the CUs (round 4 relied on sc1 stores + loads alone, valid only with one workgroup
+// per CU).  The wrong gradients that put it under suspicion (r04sf, r05c, r05d: the 2-rank sharded 70k test)
+// came from the TEST's host-staged collectives, which read device buffers before the kernels writing them
+// had finished (gnot_amd/parallel.py PointShardComm, fixed): they reproduced with this combine switched off.
+// The release costs ~1 ms per chain backward and ~2.3 ms per bf16 chain forward (it writes back the XCD L2's
+// dirty lines once per workgroup), so the default is the combine pass.
 template <bool B16>
 GNOT_DEV void moe_combine_last(const float* stage, long stage_stride, int E, const float* base, float* out,
                                int* counters, int blk, long row0, int nrows) {
@@ -142,6 +138,7 @@ GNOT_DEV void moe_combine_last(const float* stage, long stage_stride, int E, con
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     const int old = __hip_atomic_fetch_add(counters + blk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last = old == E - 1;
     if (old == E - 1) {
@@ -554,6 +551,12 @@ __global__ void __launch_bounds__(64 * kC2Waves, 2) chain2_fwd_kernel(ChainArgs 
       else store_rows_sc1<OTL>(y, make_rsrc(a.Y + e * a.y_chain_stride + row0 * D, lay_bytes), voff);
       return;
     }
+    if constexpr (B16) {
+      if (a.stage_b16 && a.Y != nullptr) {    // bf16 stage rows for the moe_combine_b16 pass
+        store_rows_b16<OTL>(y, make_rsrc(a.Y + e * a.y_chain_stride + rbase, lay_b16), rowb, lane);
+        return;
+      }
+    }
   }
   if (a.Y != nullptr) store_rows<OTL>(y, a.Y + e * a.y_chain_stride, a.ldy, p, valid, a.out_dim, lane);
   }
@@ -869,6 +872,8 @@ __global__ void __launch_bounds__(64 * kC2Waves, 2) chain2_bwd_kernel(ChainArgs 
     } else if (KT0 == 16 && a.combine != nullptr) {   // fused combine: write-through stage rows (D = 256)
       if constexpr (B16) store_rows_b16_sc1<KT0>(dx, make_rsrc(a.dX + e * a.dx_chain_stride + rbase, lay_b16), rowb, lane);
       else store_rows_sc1<KT0>(dx, make_rsrc(a.dX + e * a.dx_chain_stride + row0 * D, lay_bytes), voff);
+    } else if (B16 && KT0 == 16 && a.stage_b16) {    // bf16 stage rows for the moe_combine_b16 pass
+      store_rows_b16<KT0>(dx, make_rsrc(a.dX + e * a.dx_chain_stride + rbase, lay_b16), rowb, lane);
     } else {
       if constexpr (B16) round_rows_bf16<KT0>(dx);   // the fused combine's bf16 stage value (see the forward)
       store_rows<KT0>(dx, a.dX + e * a.dx_chain_stride, a.lddx, p, valid, a.in_dim, lane);
@@ -901,6 +906,9 @@ static hipError_t launch_chain2_d(const ChainArgs& a, bool bwd, hipStream_t s) {
   const dim3 block(64 * kC2Waves);
   if (a.combine != nullptr && (a.walk || a.mode != CH_MOE || a.KT0 != DT || a.OTL != DT || !a.counters ||
                                (bwd ? (!a.dX || a.lddx != D || a.dx_chain_stride % 4) : (!a.Y || a.ldy != D || a.y_chain_stride % 4))))
+    return hipErrorInvalidValue;
+  if (a.stage_b16 && (!a.b16s || a.walk || a.combine != nullptr ||
+                      (bwd ? (!a.dX || a.dx_chain_stride % 4) : (a.y_chain_stride % 4))))
     return hipErrorInvalidValue;
   const size_t lds = C2Lds<D, NP>::kBytes;
 #define GNOT_C2_ATTR(K)                                                                                  \

@@ -208,6 +208,8 @@ struct gnot_plan {
   // soft-MoE calls in the walk form (chain2.hip: one workgroup sums all experts in place, no [P, E, d]
   // stage): decided per batch in gnot_plan_set_batch (chain2_walk_choice)
   bool moe_walk = false;
+  // GNOT_MOE_FUSED=1 (read per batch): the opt-in fused soft-MoE combine (moe_fused)
+  bool moe_fused_env = false;
   // input gradients (gnot_plan_set_input_grads): the x / gating / input-function encoders' first Linears
   // also run their backward-data into dxin / dxg / dfnin<i>
   bool input_grads = false;
@@ -217,6 +219,9 @@ struct gnot_plan {
   // bf16 mode stores the soft-MoE chains' saves and dZ as bf16 (ChainArgs::b16s): one [P, 256] bf16 layer
   // is P * D / 2 four-byte units, a chain's 2 * NL save slots take what NL fp32 layers did
   bool b16s() const { return np == 1 && D == 256; }
+  // operand pieces of the kernels this plan runs: the bf16 mode covers every width up to 256 (chain.hip /
+  // linear.hip / the 128-tile weight gradients at d <= 192 as well); above 256 (chainw.hip) the fp32 path
+  int npk() const { return D <= 256 ? np : 3; }
   std::string msave(int l, bool m1) const {
     return moe_recompute ? std::string("mrsave") : "b" + std::to_string(l) + (m1 ? ".m1save" : ".m2save");
   }
@@ -482,22 +487,24 @@ static void plan_images(gnot_plan* p) {
     p->pack_jobs.back().W = reinterpret_cast<const float*>((intptr_t)li);
   };
   // d = 256: chain2.hip, bf16x6 output-major images in both directions; else chain.hip, k-major x6
-  // forward image + exact fp32 backward-data image
+  // forward image + exact fp32 backward-data image (bf16 mode: k-major one-piece images both ways, and the
+  // projections on output-major one-piece images, linear.hip)
   const bool c2 = p->D == 256;
   const int c2np = c2 ? p->np : 3;                 // pieces of the output-major images
   const int c2x6 = c2np == 1 ? 3 : 2;              // their pack mode
   // d > 256 (chainw.hip: each Linear on linear.hip): fp32 fragment images in both directions
   const bool cw = p->D > 256;
+  const bool b1 = !c2 && !cw && p->npk() == 1;      // d <= 192 in the bf16 mode
   auto chain_imgs = [&](int first, int KT0, int OTL) {
     for (int j = 0; j < NL; ++j) {
       const int li = first + j;
       const int KTp = (j == 0) ? KT0 : DT;
       const int OTp = (j == NL - 1) ? OTL : DT;
-      Img f = cw ? new_img(OTp, KTp) : new_img_x6(OTp, KTp, c2np);
+      Img f = cw ? new_img(OTp, KTp) : new_img_x6(OTp, KTp, c2 ? c2np : b1 ? 1 : 3);
       const size_t bo = new_bias(16 * OTp);
-      job(li, f, 0, 0, OTp, KTp, 0, (long)bo, cw ? 0 : c2 ? c2x6 : 1);
-      Img t = c2 ? new_img_x6(KTp, OTp, c2np) : new_img(KTp, OTp);   // backward-data image
-      job(li, t, 0, 0, KTp, OTp, 1, -1, c2 ? c2x6 : 0);
+      job(li, f, 0, 0, OTp, KTp, 0, (long)bo, cw ? 0 : c2 ? c2x6 : b1 ? 4 : 1);
+      Img t = c2 ? new_img_x6(KTp, OTp, c2np) : b1 ? new_img_x6(KTp, OTp, 1) : new_img(KTp, OTp);   // backward-data
+      job(li, t, 0, 0, KTp, OTp, 1, -1, c2 ? c2x6 : b1 ? 4 : 0);
       p->fwd_img[li] = f;
       p->T_img[li] = t;
       p->fwd_bias[li] = bo;
@@ -515,8 +522,8 @@ static void plan_images(gnot_plan* p) {
   auto attn_imgs = [&](gnot_plan::AttnImgs& A, int iq, int io, const std::vector<int>& ik,
                        const std::vector<int>& iv, bool selftype) {
     const int D = p->D;
-    const int x6 = c2 ? c2x6 : 0;
-    auto img = [&](int OT, int KT) { return c2 ? new_img_x6(OT, KT, c2np) : new_img(OT, KT); };
+    const int x6 = c2 ? c2x6 : b1 ? 3 : 0;
+    auto img = [&](int OT, int KT) { return c2 ? new_img_x6(OT, KT, c2np) : b1 ? new_img_x6(OT, KT, 1) : new_img(OT, KT); };
     if (selftype) {
       A.qkv = img(3 * DT, DT);
       A.bqkv = new_bias(3 * D);
@@ -1173,6 +1180,10 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
     C.add(s + "query2", P * D, D);
   }
   p->moe_walk = p->D == 256 && p->L > 0 && chain2_walk_choice(P, E);
+  {
+    const char* f = std::getenv("GNOT_MOE_FUSED");
+    p->moe_fused_env = f && f[0] == '1';
+  }
   if (!p->moe_walk) C.add("stage", E * P * D, D);
   if (D > 256) {                             // chainw.hip scratch: query-branch chains / input-function branch
     C.add("lw_scr", 2 * P * D, D);
@@ -1504,7 +1515,7 @@ int run_linear(Ctx& c, const float* X, long ldx, int K, const Img& A, const floa
   LinearArgs a{};
   a.nseg = 1; a.X[0] = X; a.Wp[0] = A.p; a.ldx = ldx; a.nsum = 1; a.sum_stride = 0; a.K = K;
   a.bias = bias; a.Y = Y; a.ldy = ldy; a.NO = NO; a.P = (int)P;
-  a.epi = epi; a.nsoft = nsoft; a.dh = c.p->dh; a.np = c.p->np;
+  a.epi = epi; a.nsoft = nsoft; a.dh = c.p->dh; a.np = c.p->npk();
   a.dreal = (nsoft > 0 && c.p->padded()) ? c.p->Dr : 0;
   a.ncol = ncol;
   GNOT_CK(c.p->D == 256 ? launch_linear2(a, c.s) : launch_linear(a, c.p->D, c.s));
@@ -1522,7 +1533,7 @@ int run_linear_seg(Ctx& c, std::initializer_list<std::pair<const float*, const I
     ++a.nseg;
   }
   a.ldx = ldx; a.nsum = 1; a.K = c.p->D; a.bias = nullptr; a.Y = Y; a.ldy = ldy; a.NO = c.p->D; a.P = (int)P;
-  a.epi = epi; a.nsoft = 0; a.dh = c.p->dh; a.np = c.p->np;
+  a.epi = epi; a.nsoft = 0; a.dh = c.p->dh; a.np = c.p->npk();
   GNOT_CK(c.p->D == 256 ? launch_linear2(a, c.s) : launch_linear(a, c.p->D, c.s));
   return GNOT_OK;
 }
@@ -1539,7 +1550,7 @@ ChainArgs chain_args(gnot_plan* p, const ChainTable& T, long P) {
   a.D = p->D; a.KT0 = T.KT0; a.OTL = T.OTL; a.nlin = p->NL;
   a.layers_host = T.host.data();
   a.in_dim = T.in_dim; a.out_dim = T.out_dim; a.P = (int)P; a.nchains = T.nchains; a.layers = T.dev;
-  a.np = p->np;
+  a.np = p->npk();
   return a;
 }
 
@@ -1588,7 +1599,7 @@ int launch_group(gnot_plan* p, const WgradGroup& G, float* slab, hipStream_t s) 
                              slab, s));
   else
     GNOT_CK(launch_wgrad(G.d_jobs, G.d_wg_prefix, (int)G.jobs.size(), G.total_wgs, G.d_red_prefix, G.total_red, slab,
-                         s, G.x6, G.wide, p->np));
+                         s, G.x6, G.wide, p->npk()));
   return GNOT_OK;
 }
 
@@ -1794,14 +1805,24 @@ int attn_backward(Ctx& c, int l, bool cross) {
 // (262,144 points, E = 8; profiles/r04_chain_grid.txt): bf16x6 forward 6.76 ms + 0.47 pass against 7.51
 // fused, backward 8.27 + 0.47 against 8.73; bf16 storage forward 4.01 + 0.47 against 4.08 fused
 static bool moe_walk(gnot_plan* p) { return p->moe_walk; }
-// The expert grid's fused combine hands a block's stage rows to its last workgroup with write-through
-// stores and loads, the form MI355X_MICROARCH.md validates with one workgroup per CU.  A plan that forks
-// its weight gradients onto the side stream (below kWgradSerialPoints) can have small side-stream
-// workgroups co-resident with the chain's, outside that form, so it sums the stage with the combine pass
-// (no hand-off; bitwise the same results, tests/test_gpu_recompute.py).  The walk form, its round-4
-// choice for those plans, made configs[0] 15 % slower (9.6 -> 11.0 ms per step).
+// The expert grid's fused combine (an inter-workgroup hand-off of a block's stage rows to its last
+// workgroup, chain2.hip moe_combine_last) is OPT-IN since round 5 (GNOT_MOE_FUSED=1, read per batch, plans
+// with serial weight gradients).  In the guide's general form (agent release before the counter add, agent
+// acquire in the last workgroup) it is valid beside any co-resident work, but the release writes back the
+// XCD L2's dirty lines of every workgroup: measured on one box, interleaved x2 (profiles/r05h_*), fp32 chain
+// backward 10.24 / 10.27 ms fused vs 9.18 / 9.19 + the pass, step 238.7 / 239.3 vs 234.2 / 234.9 ms; bf16
+// mode 122.6 / 122.7 vs 97.4 / 97.0 ms.  So every soft-MoE call sums its stage with the moe_combine pass --
+// a kernel boundary, no hand-off (the bf16 mode over bf16 stage rows, moe_combine_b16).  Every form gives the
+// same bits (tests/test_gpu_moe_walk.py, test_gpu_recompute.py)
 static bool moe_fused(gnot_plan* p, bool bwd) {
-  return p->D == 256 && !p->moe_walk && p->serial_wgrad() && (bwd || p->b16s());
+  return p->moe_fused_env && p->D == 256 && !p->moe_walk && p->serial_wgrad() && (bwd || p->b16s());
+}
+// the bf16 mode's expert grid with the combine pass: bf16 stage rows and moe_combine_b16
+static bool moe_stage_b16(gnot_plan* p, bool bwd) { return p->b16s() && !p->moe_walk && !moe_fused(p, bwd); }
+static hipError_t launch_moe_pass(gnot_plan* p, const float* base, const float* stage, float* out, hipStream_t s) {
+  const long P = p->P, D = p->D;
+  return p->b16s() ? launch_moe_combine_b16(base, stage, P * D, p->E, out, P, s)
+                   : launch_moe_combine(base, stage, P * D, p->E, out, P * D, s);
 }
 // save (and dZ) layout of a soft-MoE chain call: fp32 [NL][P][D] per expert, or in bf16 mode 2 NL bf16
 // layers per expert (ChainArgs::b16s)
@@ -1827,12 +1848,13 @@ static int moe_forward(Ctx& c, const ChainTable& T, const float* in, const float
   } else {
     a.Y = p->P_("stage"); a.y_chain_stride = P * D;
     if (moe_fused(p, false)) { a.base = qin; a.combine = qout; a.counters = reinterpret_cast<int*>(p->P_("moe_cnt")); }
+    a.stage_b16 = moe_stage_b16(p, false) ? 1 : 0;
   }
   {
     ProfScope ps(c, "moe_fwd", 2.0 * E * P * NL * (double)D * D);
     GNOT_CK(launch_chain_fwd(cw_scratch(p, a, c.s), c.s));
   }
-  if (!walk && !moe_fused(p, false)) GNOT_CK(launch_moe_combine(qin, p->P_("stage"), P * D, E, qout, P * D, c.s));
+  if (!walk && !moe_fused(p, false)) GNOT_CK(launch_moe_pass(p, qin, p->P_("stage"), qout, c.s));
   return GNOT_OK;
 }
 
@@ -2013,9 +2035,10 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
       } else {
         a.dX = stage; a.lddx = D; a.dx_chain_stride = P * D;
         if (moe_fused(p, true)) { a.combine = dsum; a.counters = reinterpret_cast<int*>(p->P_("moe_cnt")); }
+        a.stage_b16 = moe_stage_b16(p, true) ? 1 : 0;
       }
       GNOT_RUN(chain_bwd(a, m1 ? p->k_m1(l) : p->k_m2(l), P, m1 ? p->wg_m1[l] : p->wg_m2[l], "moe_bwd"));
-      if (!walk && !moe_fused(p, true)) GNOT_CK(launch_moe_combine(nullptr, stage, P * D, E, dsum, P * D, c.s));
+      if (!walk && !moe_fused(p, true)) GNOT_CK(launch_moe_pass(p, nullptr, stage, dsum, c.s));
       // m2: self attention (model.py:133) ; m1: cross attention (model.py:127)
       GNOT_RUN(attn_backward(c, l, m1));
     }

@@ -300,22 +300,23 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int x6_buf_kb(int) { return 24; }
 constexpr int x6_buf_f4(int D) { return x6_buf_kb(D) * WAVE; }   // 16-byte units per buffer
 
-template <int D>
-constexpr int x6_och(int KT, int OT) {                // output tiles per chunk (3 KiB per block)
+// NP: pieces per block (3: bf16x6, 1: one RNE bf16 piece, the bf16 arithmetic mode; pack x6 = 1 / 4)
+template <int D, int NP = 3>
+constexpr int x6_och(int KT, int OT) {                // output tiles per chunk (NP KiB per block)
   int c = OT;
-  while (c > 1 && (c * 3 > x6_buf_kb(D) || OT % c != 0)) --c;
+  while (c > 1 && (c * NP > x6_buf_kb(D) || OT % c != 0)) --c;
   return c;
 }
-template <int D>
+template <int D, int NP = 3>
 constexpr int x6_tch(int KT, int OT) {                // k-blocks per chunk
   const int KB = (KT + 1) / 2;
-  if (x6_och<D>(KT, OT) != OT) return 1;
+  if (x6_och<D, NP>(KT, OT) != OT) return 1;
   int c = KB;
-  while (c > 1 && (c * OT * 3 > x6_buf_kb(D) || KB % c != 0)) --c;
+  while (c > 1 && (c * OT * NP > x6_buf_kb(D) || KB % c != 0)) --c;
   return c;
 }
-template <int D>
-constexpr int x6_chunk_f4(int KT, int OT) { return x6_och<D>(KT, OT) * x6_tch<D>(KT, OT) * 3 * WAVE; }
+template <int D, int NP = 3>
+constexpr int x6_chunk_f4(int KT, int OT) { return x6_och<D, NP>(KT, OT) * x6_tch<D, NP>(KT, OT) * NP * WAVE; }
 
 GNOT_DEV unsigned f2u(float x) { return __builtin_bit_cast(unsigned, x); }
 // (hi & 0xFFFF0000) | (lo >> 16) in one v_perm_b32: the high halves of two words as two bf16
@@ -478,23 +479,24 @@ GNOT_DEV f32x4 mfma_bf16(const u32x4& a, const u32x4& b, f32x4 c) {
 // 2*x6_buf_f4 units, next image staged across the layer boundary, hook after the first chunk's
 // barrier), for k-major x6 weight images.  Per 16x16x32 block the six order <= 2 products go into
 // the tile's one accumulator, smallest terms first (a single accumulation chain of
-// v_mfma_f32_16x16x32_bf16 issues at full rate, MI355X_MICROARCH.md).
-template <int D, int KT, int OT, typename Hook = NoHook>
+// v_mfma_f32_16x16x32_bf16 issues at full rate, MI355X_MICROARCH.md).  NP = 1 (bf16 mode, one-piece
+// k-major images, pack x6 = 4): one product per block, the input rounded to bf16 (RNE).
+template <int D, int KT, int OT, int NP = 3, typename Hook = NoHook>
 GNOT_DEV void mm_tiles_pipe_x6(const float4* __restrict__ Wg, const float4* __restrict__ next_W, int next_f4,
                                float4* lds, int& cnt, const float (&in)[KT][4], f32x4 (&acc)[OT], int nwaves,
                                int wave, int lane, Hook hook = Hook()) {
   constexpr int kBufF4 = x6_buf_f4(D);
   constexpr int KB = (KT + 1) / 2;
-  constexpr int OCH = x6_och<D>(KT, OT);
-  constexpr int TCH = x6_tch<D>(KT, OT);
+  constexpr int OCH = x6_och<D, NP>(KT, OT);
+  constexpr int TCH = x6_tch<D, NP>(KT, OT);
   constexpr int NOG = OT / OCH;
   constexpr int NTG = KB / TCH;
-  constexpr int CH4 = OCH * TCH * 3 * WAVE;
+  constexpr int CH4 = OCH * TCH * NP * WAVE;
 #pragma unroll
   for (int tg = 0; tg < NTG; ++tg) {
-    u32x4 bp[TCH][3];
+    u32x4 bp[TCH][NP];
 #pragma unroll
-    for (int tt = 0; tt < TCH; ++tt) split_block_x6<KT>(in, tg * TCH + tt, bp[tt]);
+    for (int tt = 0; tt < TCH; ++tt) split_block_x6<KT, NP>(in, tg * TCH + tt, bp[tt]);
 #pragma unroll
     for (int og = 0; og < NOG; ++og) {
       const int c = tg * NOG + og;
@@ -509,15 +511,17 @@ GNOT_DEV void mm_tiles_pipe_x6(const float4* __restrict__ Wg, const float4* __re
       for (int tt = 0; tt < TCH; ++tt)
 #pragma unroll
         for (int o = 0; o < OCH; ++o) {
-          u32x4 a[3];
+          u32x4 a[NP];
 #pragma unroll
-          for (int q = 0; q < 3; ++q) a[q] = cb[((tt * OCH + o) * 3 + q) * WAVE + lane];
+          for (int q = 0; q < NP; ++q) a[q] = cb[((tt * OCH + o) * NP + q) * WAVE + lane];
           f32x4 r = acc[og * OCH + o];
-          r = mfma_bf16(a[2], bp[tt][0], r);
-          r = mfma_bf16(a[1], bp[tt][1], r);
-          r = mfma_bf16(a[0], bp[tt][2], r);
-          r = mfma_bf16(a[1], bp[tt][0], r);
-          r = mfma_bf16(a[0], bp[tt][1], r);
+          if constexpr (NP == 3) {
+            r = mfma_bf16(a[2], bp[tt][0], r);
+            r = mfma_bf16(a[1], bp[tt][1], r);
+            r = mfma_bf16(a[0], bp[tt][2], r);
+            r = mfma_bf16(a[1], bp[tt][0], r);
+            r = mfma_bf16(a[0], bp[tt][1], r);
+          }
           r = mfma_bf16(a[0], bp[tt][0], r);
           acc[og * OCH + o] = r;
         }

@@ -23,7 +23,8 @@ struct PackJob {
   int o0, t0, ktot;
   int OTp, KTp;        // tile counts of this job's image (>= what out/in need; the rest is zero)
   int x6;              // 1: bf16x6 image (3 bf16 pieces per 16x32 block, k-major, gnot_common.h); 2: the
-                       //    same output-major (chain2.hip); 3: output-major, 1 RNE bf16 piece; 0: fp32
+                       //    same output-major (chain2.hip); 3: output-major, 1 RNE bf16 piece; 4: k-major,
+                       //    1 RNE bf16 piece (chain.hip in the bf16 mode); 0: fp32
   int otot;            // x6: output tiles of the whole image (its k-major block stride)
 };
 // pack tiles of a job: fp32 images have OTp*KTp tiles, x6 images OTp*ceil(KTp/2) blocks
@@ -126,6 +127,10 @@ struct ChainArgs {
   // MFMA operand the forward used), written for the weight gradients; slot nlin + 0 (the shared MoE
   // input) only in chain 0.
   int b16s = 0;
+  // b16s expert grid without the fused combine: the stage terms (forward s_e y_e, backward dX_e) go to the
+  // [E, P, d] stage as bf16 pair-interleaved rows (plain stores; the strides are the fp32 stage's), summed by
+  // launch_moe_combine_b16
+  int stage_b16 = 0;
 };
 // walk or per-expert grid for a MoE call of P points (env GNOT_MOE_WALK = 0 / 1 forces, read per call)
 bool chain2_walk_choice(long P, int E);
@@ -232,6 +237,10 @@ hipError_t launch_concat_theta(const float* x, long ldx, int in_dim, const float
 // out = (base ? base : 0) + sum_e stage[e]
 hipError_t launch_moe_combine(const float* base, const float* stage, long stage_stride, int E,
                               float* out, long n, hipStream_t s);
+// the same over bf16 pair-interleaved stage rows (ChainArgs::stage_b16: 512 B per point at the start of each
+// expert's fp32-sized region, stage_stride in floats); base / out fp32 [P, 256]
+hipError_t launch_moe_combine_b16(const float* base, const float* stage, long stage_stride, int E, float* out,
+                                  long P, hipStream_t s);
 // out[r][c] = a[r][c] + b[r][c] (b null: a copy), c < cols, out dense [rows, cols]
 hipError_t launch_add_cols(const float* a, long lda, const float* b, long ldb, int cols, float* out, long rows,
                            hipStream_t s);

@@ -17,17 +17,58 @@
 
 namespace gnot {
 
-template <int D, int OC>   // OC: output tiles per workgroup (grid.y splits NO)
+// bf16 arithmetic mode (NP = 1): the images are OUTPUT-MAJOR one-piece bf16 (pack x6 = 3, as linear2.hip's):
+// block (o, kb) = 16 outputs x 32 contraction slots at Wg[(o * KB + kb) * 64 + lane], so a workgroup's OC
+// output tiles are one contiguous run of OC * KB blocks.  Chunks of OCH tiles (OCH * KB <= 16 blocks = one
+// 16 KiB buffer) stream through the same two LDS buffers as the fp32 pipe; the input is rounded to bf16
+// once per segment (bp, one 16x16x32 B operand per k-block), one v_mfma_f32_16x16x32_bf16 per block
+constexpr int b1_och(int KB, int OC) {
+  int c = OC;
+  while (c > 1 && (c * KB > kChunkKB || OC % c != 0)) --c;
+  return c;
+}
+constexpr int b1_chunk_f4(int KB, int OC) { return b1_och(KB, OC) * KB * WAVE; }
+template <int KB, int OC, typename Hook = NoHook>
+GNOT_DEV void mm_tiles_pipe_b1(const float4* __restrict__ Wg, const float4* __restrict__ next_W, int next_f4,
+                               float4* lds, int& cnt, const u32x4 (&bp)[KB], f32x4 (&acc)[OC], int nwaves, int wave,
+                               int lane, Hook hook = Hook()) {
+  constexpr int OCH = b1_och(KB, OC);
+  constexpr int NC = OC / OCH;
+  constexpr int CH4 = OCH * KB * WAVE;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    lds_dma_wait();                                    // this chunk's DMA (issued one chunk ago) has landed
+    __syncthreads();
+    float4* nb = lds + ((cnt + 1) & 1) * kChunkF4;
+    if (c + 1 < NC) stage_image(nb, Wg + (c + 1) * CH4, CH4, nwaves, wave, lane);
+    else if (next_W) stage_image(nb, next_W, next_f4, nwaves, wave, lane);
+    if (c == 0) hook();
+    const u32x4* cb = reinterpret_cast<const u32x4*>(lds + (cnt & 1) * kChunkF4);
+#pragma unroll
+    for (int o = 0; o < OCH; ++o) {
+      f32x4 r = acc[c * OCH + o];
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) r = mfma_bf16(cb[(o * KB + kb) * WAVE + lane], bp[kb], r);
+      acc[c * OCH + o] = r;
+    }
+    ++cnt;
+  }
+}
+
+template <int D, int OC, int NP = 3>   // OC: output tiles per workgroup (grid.y splits NO)
 GNOT_DEV void linear_body(const LinearArgs& a, float4* wlds) {
-  constexpr int KT = D / 16;
+  constexpr int KT = D / 16, KB = (KT + 1) / 2;
+  constexpr bool B1 = NP == 1;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const long p = ((long)blockIdx.x * 4 + wave) * 16 + (lane & 15);
   const bool valid = p < a.P;
   const int c = blockIdx.y;                       // output chunk of this workgroup
-  const long wchunk = (long)c * OC * KT * WAVE;   // chunk offset inside every segment's image
+  // chunk offset inside every segment's image (fp32 tiles of KT x 1 KiB, or KB one-piece blocks per tile)
+  const long wchunk = (long)c * OC * (B1 ? KB : KT) * WAVE;
+  const int cf4 = B1 ? b1_chunk_f4(KB, OC) : chunk_f4(KT, OC);
   int cnt = 0;
-  stage_image(wlds, a.Wp[0] + wchunk, chunk_f4(KT, OC), 4, wave, lane);
+  stage_image(wlds, a.Wp[0] + wchunk, cf4, 4, wave, lane);
 
   // segment 0 input (optionally the sum of nsum equally strided buffers)
   float in[KT][4];
@@ -50,8 +91,20 @@ GNOT_DEV void linear_body(const LinearArgs& a, float4* wlds) {
     auto pre = [&]() {
       if (more) load_rows<KT>(nx, a.X[sg + 1], a.ldx, p, valid, a.K, lane);
     };
-    mm_tiles_pipe<KT, OC>(a.Wp[sg] + wchunk, more ? a.Wp[sg + 1] + wchunk : nullptr, chunk_f4(KT, OC), wlds, cnt,
-                          in, acc, 4, wave, lane, pre);
+    if constexpr (B1) {
+      u32x4 bp[KB];
+#pragma unroll
+      for (int kb = 0; kb < KB; ++kb) {
+        u32x4 t[1];
+        split_block_x6<KT, 1>(in, kb, t);
+        bp[kb] = t[0];
+      }
+      mm_tiles_pipe_b1<KB, OC>(a.Wp[sg] + wchunk, more ? a.Wp[sg + 1] + wchunk : nullptr, cf4, wlds, cnt, bp, acc, 4,
+                               wave, lane, pre);
+    } else {
+      mm_tiles_pipe<KT, OC>(a.Wp[sg] + wchunk, more ? a.Wp[sg + 1] + wchunk : nullptr, cf4, wlds, cnt, in, acc, 4,
+                            wave, lane, pre);
+    }
     if (more) {
 #pragma unroll
       for (int T = 0; T < KT; ++T)
@@ -84,10 +137,10 @@ GNOT_DEV void linear_body(const LinearArgs& a, float4* wlds) {
   store_rows<OC>(h, Y, a.ldy, p, valid, ncols, lane);
 }
 
-template <int D, int OC>
+template <int D, int OC, int NP = 3>
 __global__ void __launch_bounds__(256) linear_kernel(LinearArgs a) {
   __shared__ __attribute__((aligned(16))) float4 wlds[2 * pipe_buf_f4<D / 16>()];
-  linear_body<D, OC>(a, wlds);
+  linear_body<D, OC, NP>(a, wlds);
 }
 
 // several independent projections in one launch: job = blockIdx.z (jobs live in device memory)
@@ -138,6 +191,15 @@ int linear_oc(int D, int NO, int nsoft, int dh) {
   GNOT_LIN(256, 2) GNOT_LIN(256, 4) GNOT_LIN(256, 8) GNOT_LIN(320, 1) GNOT_LIN(320, 2) GNOT_LIN(320, 4)   \
   GNOT_LIN(384, 1) GNOT_LIN(384, 2) GNOT_LIN(384, 4) GNOT_LIN(448, 1) GNOT_LIN(448, 2) GNOT_LIN(448, 4)   \
   GNOT_LIN(512, 1) GNOT_LIN(512, 2) GNOT_LIN(512, 4)
+// the d <= 192 cases of GNOT_LIN_CASES (the bf16 mode's one-piece kernels)
+#define GNOT_LIN_B1_CASES                                                                                         \
+  GNOT_LIN_B1(16, 1) GNOT_LIN_B1(32, 1) GNOT_LIN_B1(32, 2) GNOT_LIN_B1(48, 1) GNOT_LIN_B1(48, 3) GNOT_LIN_B1(64, 1)   \
+  GNOT_LIN_B1(64, 2) GNOT_LIN_B1(64, 4) GNOT_LIN_B1(80, 1) GNOT_LIN_B1(80, 5) GNOT_LIN_B1(96, 1) GNOT_LIN_B1(96, 2)   \
+  GNOT_LIN_B1(96, 3) GNOT_LIN_B1(96, 6) GNOT_LIN_B1(112, 1) GNOT_LIN_B1(112, 7) GNOT_LIN_B1(128, 1)                   \
+  GNOT_LIN_B1(128, 2) GNOT_LIN_B1(128, 4) GNOT_LIN_B1(128, 8) GNOT_LIN_B1(144, 1) GNOT_LIN_B1(144, 3)                  \
+  GNOT_LIN_B1(144, 9) GNOT_LIN_B1(160, 1) GNOT_LIN_B1(160, 2) GNOT_LIN_B1(160, 5) GNOT_LIN_B1(160, 10)                \
+  GNOT_LIN_B1(176, 1) GNOT_LIN_B1(176, 11) GNOT_LIN_B1(192, 1) GNOT_LIN_B1(192, 2) GNOT_LIN_B1(192, 3)                 \
+  GNOT_LIN_B1(192, 4) GNOT_LIN_B1(192, 6) GNOT_LIN_B1(192, 12)
 
 hipError_t launch_linear(const LinearArgs& a, int D, hipStream_t s) {
   if (a.P <= 0) return hipSuccess;
@@ -146,8 +208,20 @@ hipError_t launch_linear(const LinearArgs& a, int D, hipStream_t s) {
   const dim3 grid((a.P + 63) / 64, a.NO / (16 * oc)), block(256);
 #define GNOT_LIN(DD, OO) \
   if (D == DD && oc == OO) { hipLaunchKernelGGL((linear_kernel<DD, OO>), grid, block, 0, s, a); return hipGetLastError(); }
+  // bf16 mode (a.np == 1) at d <= 192: one-piece output-major images (the d = 256 projections are linear2.hip's)
+#define GNOT_LIN_B1(DD, OO)                                                                              \
+  if (D == DD && oc == OO) {                                                                              \
+    hipLaunchKernelGGL((linear_kernel<DD, OO, 1>), grid, block, 0, s, a);                                 \
+    return hipGetLastError();                                                                             \
+  }
+  if (a.np == 1) {
+    if (D > 192) return hipErrorInvalidValue;
+    GNOT_LIN_B1_CASES
+    return hipErrorInvalidValue;
+  }
   GNOT_LIN_CASES
 #undef GNOT_LIN
+#undef GNOT_LIN_B1
   return hipErrorInvalidValue;
 }
 

@@ -70,6 +70,40 @@ hipError_t launch_moe_combine(const float* base, const float* stage, long stage_
   return hipGetLastError();
 }
 
+// bf16 stage rows: thread = one 16-byte chunk k of a point's 512-byte pair-interleaved row (gnot_common.h
+// b16_off): features f0 .. f0+3 (half 0) and f0+16 .. f0+19 (half 1), f0 = 32 (k >> 2) + 4 (k & 3).  Sums in
+// expert order from base, as moe_combine does over the same (bf16-exact) values: bitwise equal to it
+__global__ void __launch_bounds__(256) moe_combine_b16_kernel(const float* __restrict__ base,
+                                                              const float* __restrict__ stage, long stage_stride,
+                                                              int E, float* __restrict__ out, long P) {
+  const long nch = P * 32;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < nch; i += (long)gridDim.x * 256) {
+    const long pnt = i >> 5;
+    const int k = (int)(i & 31), f0 = 32 * (k >> 2) + 4 * (k & 3);
+    const long fo = pnt * 256 + f0;
+    float4 lo = base ? *reinterpret_cast<const float4*>(base + fo) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 hi = base ? *reinterpret_cast<const float4*>(base + fo + 16) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* sp = stage + pnt * (kB16Row / 4) + 4 * k;
+    for (int e = 0; e < E; ++e) {
+      const u32x4 w = *reinterpret_cast<const u32x4*>(sp + e * stage_stride);
+      lo.x += bf16_lo(w[0]); lo.y += bf16_hi(w[0]); lo.z += bf16_lo(w[1]); lo.w += bf16_hi(w[1]);
+      hi.x += bf16_lo(w[2]); hi.y += bf16_hi(w[2]); hi.z += bf16_lo(w[3]); hi.w += bf16_hi(w[3]);
+    }
+    *reinterpret_cast<float4*>(out + fo) = lo;
+    *reinterpret_cast<float4*>(out + fo + 16) = hi;
+  }
+}
+
+hipError_t launch_moe_combine_b16(const float* base, const float* stage, long stage_stride, int E, float* out,
+                                  long P, hipStream_t s) {
+  if (P <= 0) return hipSuccess;
+  if (stage_stride & 3) return hipErrorInvalidValue;
+  const long blocks = std::min<long>((P * 32 + 255) / 256, 8192);
+  hipLaunchKernelGGL(moe_combine_b16_kernel, dim3((unsigned)blocks), dim3(256), 0, s, base, stage, stage_stride, E,
+                     out, P);
+  return hipGetLastError();
+}
+
 __global__ void __launch_bounds__(256) segcopy_kernel(const CopySeg* __restrict__ segs, const int* __restrict__ prefix4,
                                                       int nseg, int total4, const float* __restrict__ src,
                                                       float* __restrict__ dst, int reverse) {

@@ -30,8 +30,8 @@ __global__ void __launch_bounds__(64) pack_kernel(const PackJob* __restrict__ jo
   if (J.x6) {
     // bf16x6 image block (o, kb): lane holds row 16o + r16 at k-slots 8g + j of k-block kb; blocks are
     // k-major (x6 = 1: chain.hip, a k-block of every output tile together) or output-major (x6 = 2:
-    // chain2.hip / linear2.hip, an output tile's k-blocks together); x6 = 3: output-major with ONE
-    // RNE bf16 piece (the bf16 arithmetic mode)
+    // chain2.hip / linear2.hip / linear.hip, an output tile's k-blocks together); x6 = 3 / 4: output-major /
+    // k-major with ONE RNE bf16 piece (the bf16 arithmetic mode)
     const int KB = (J.KTp + 1) / 2;
     const int o = t / KB, kb = t % KB;
     unsigned w[3][8];
@@ -51,9 +51,10 @@ __global__ void __launch_bounds__(64) pack_kernel(const PackJob* __restrict__ jo
       w[2][j] = __builtin_bit_cast(unsigned, r2);
     }
     uint4* dst = reinterpret_cast<uint4*>(J.dst);
-    const long blk = J.x6 >= 2 ? (long)(J.o0 + o) * ((J.ktot + 1) / 2) + J.t0 / 2 + kb    // output-major
-                               : (long)(J.t0 / 2 + kb) * J.otot + J.o0 + o;               // k-major
-    if (J.x6 == 3) {
+    const bool omaj = J.x6 == 2 || J.x6 == 3;
+    const long blk = omaj ? (long)(J.o0 + o) * ((J.ktot + 1) / 2) + J.t0 / 2 + kb    // output-major
+                          : (long)(J.t0 / 2 + kb) * J.otot + J.o0 + o;               // k-major
+    if (J.x6 >= 3) {
       // bf16 arithmetic mode: one round-to-nearest-even piece (w[0] holds the fp32 bits)
       uint4 u;
       u.x = (bf16_rne_bits(u2f(w[0][1])) << 16) | bf16_rne_bits(u2f(w[0][0]));

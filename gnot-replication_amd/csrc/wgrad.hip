@@ -230,10 +230,29 @@ GNOT_DEV void x6_load8x2(float (&v)[2][8], const float* base, long ld, long prow
   }
 }
 
+GNOT_DEV void x6_mfma6(const u32x4 (&a)[3], const u32x4 (&b)[3], f32x16& c) {
+#define GNOT_MFMA32(X, Y) \
+  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, X), __builtin_bit_cast(bf16x8, Y), c, 0, 0, 0)
+  GNOT_MFMA32(a[2], b[0]);
+  GNOT_MFMA32(a[1], b[1]);
+  GNOT_MFMA32(a[0], b[2]);
+  GNOT_MFMA32(a[1], b[0]);
+  GNOT_MFMA32(a[0], b[1]);
+  GNOT_MFMA32(a[0], b[0]);
+#undef GNOT_MFMA32
+}
+template <int NP>
+GNOT_DEV void mfma_np(const u32x4 (&a)[NP], const u32x4 (&b)[NP], f32x16& c) {
+  if constexpr (NP == 3) x6_mfma6(a, b, c);
+  else c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[0]), __builtin_bit_cast(bf16x8, b[0]), c, 0, 0, 0);
+}
+
+// NP = 1 (bf16 mode): one RNE bf16 piece per operand and one MFMA per 32x32x16 block
+template <int NP>
 __global__ void __launch_bounds__(256) pgemm_x6_kernel(const WgradJob* __restrict__ jobs,
                                                        const int* __restrict__ prefix, int njobs,
                                                        float* __restrict__ slab) {
-  __shared__ __attribute__((aligned(16))) unsigned short lds[2 * 3 * kX6Piece];
+  __shared__ __attribute__((aligned(16))) unsigned short lds[2 * NP * kX6Piece];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int j = find_job(prefix, njobs, blockIdx.x);
@@ -281,14 +300,14 @@ __global__ void __launch_bounds__(256) pgemm_x6_kernel(const WgradJob* __restric
         vb[k] = gel ? gelu(rb[jf][k]) : rb[jf][k];
         dbacc[jf] += ra[jf][k];
       }
-      u32x4 pa[3], pbv[3];
-      split8_x6(ra[jf], pa);
-      split8_x6(vb, pbv);
+      u32x4 pa[NP], pbv[NP];
+      split8_np<NP>(ra[jf], pa);
+      split8_np<NP>(vb, pbv);
       const int f = 2 * fp + jf;
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
+      for (int q = 0; q < NP; ++q) {
         *reinterpret_cast<u32x4*>(lds + q * kX6Piece + f * kX6Row + 8 * o) = pa[q];
-        *reinterpret_cast<u32x4*>(lds + (3 + q) * kX6Piece + f * kX6Row + 8 * o) = pbv[q];
+        *reinterpret_cast<u32x4*>(lds + (NP + q) * kX6Piece + f * kX6Row + 8 * o) = pbv[q];
       }
       asm volatile("" ::: "memory");          // one feature at a time: bounds the staging registers
     }
@@ -297,29 +316,18 @@ __global__ void __launch_bounds__(256) pgemm_x6_kernel(const WgradJob* __restric
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int koff = 16 * ks + 8 * h;
-      u32x4 af[2][3], bf[2][3];
+      u32x4 af[2][NP], bf[2][NP];
 #pragma unroll
       for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int q = 0; q < 3; ++q) {
+        for (int q = 0; q < NP; ++q) {
           af[a][q] = *reinterpret_cast<const u32x4*>(lds + q * kX6Piece + (wo * 64 + a * 32 + r32) * kX6Row + koff);
-          bf[a][q] = *reinterpret_cast<const u32x4*>(lds + (3 + q) * kX6Piece + (wi * 64 + a * 32 + r32) * kX6Row + koff);
+          bf[a][q] = *reinterpret_cast<const u32x4*>(lds + (NP + q) * kX6Piece + (wi * 64 + a * 32 + r32) * kX6Row + koff);
         }
 #pragma unroll
       for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-#define GNOT_MFMA32(X, Y, C) \
-  C = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, X), __builtin_bit_cast(bf16x8, Y), C, 0, 0, 0)
-          // smallest terms first
-          GNOT_MFMA32(af[a][2], bf[b][0], acc[a][b]);
-          GNOT_MFMA32(af[a][1], bf[b][1], acc[a][b]);
-          GNOT_MFMA32(af[a][0], bf[b][2], acc[a][b]);
-          GNOT_MFMA32(af[a][1], bf[b][0], acc[a][b]);
-          GNOT_MFMA32(af[a][0], bf[b][1], acc[a][b]);
-          GNOT_MFMA32(af[a][0], bf[b][0], acc[a][b]);
-#undef GNOT_MFMA32
-        }
+        for (int b = 0; b < 2; ++b) mfma_np<NP>(af[a], bf[b], acc[a][b]);   // smallest terms first
       asm volatile("" ::: "memory");          // k-step 1's fragments are not hoisted over k-step 0
     }
   }
@@ -380,23 +388,6 @@ constexpr int kWRawSlot = 2 * 2 * 64;            // u32x4 per wave-private raw s
 constexpr int kWRawSlots = 2;
 // LDS: two fragment buffers | 8 waves x 2 raw slots (96 + 64 = 160 KiB at NP = 3)
 constexpr size_t w_lds_bytes(int np) { return (2 * (size_t)w_buf(np) + 8 * kWRawSlots * kWRawSlot) * 16; }
-
-GNOT_DEV void x6_mfma6(const u32x4 (&a)[3], const u32x4 (&b)[3], f32x16& c) {
-#define GNOT_MFMA32(X, Y) \
-  c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, X), __builtin_bit_cast(bf16x8, Y), c, 0, 0, 0)
-  GNOT_MFMA32(a[2], b[0]);
-  GNOT_MFMA32(a[1], b[1]);
-  GNOT_MFMA32(a[0], b[2]);
-  GNOT_MFMA32(a[1], b[0]);
-  GNOT_MFMA32(a[0], b[1]);
-  GNOT_MFMA32(a[0], b[0]);
-#undef GNOT_MFMA32
-}
-template <int NP>
-GNOT_DEV void mfma_np(const u32x4 (&a)[NP], const u32x4 (&b)[NP], f32x16& c) {
-  if constexpr (NP == 3) x6_mfma6(a, b, c);
-  else c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[0]), __builtin_bit_cast(bf16x8, b[0]), c, 0, 0, 0);
-}
 
 // one dword of a wave-private raw slot (inline asm: the compiler does not order it against the LDS-DMA
 // still in flight to the OTHER slot; the caller's counted vmcnt already retired this slot's DMA, and a
@@ -879,8 +870,10 @@ hipError_t launch_wgrad(const WgradJob* jobs_dev, const int* wg_prefix_dev, int 
   }
     GNOT_X6W(3) GNOT_X6W(1)
 #undef GNOT_X6W
-  } else if (x6)
-    hipLaunchKernelGGL(pgemm_x6_kernel, dim3(total_wgs), dim3(256), 0, s, jobs_dev, wg_prefix_dev, njobs, slab);
+  } else if (x6) {
+    if (np == 1) hipLaunchKernelGGL(pgemm_x6_kernel<1>, dim3(total_wgs), dim3(256), 0, s, jobs_dev, wg_prefix_dev, njobs, slab);
+    else hipLaunchKernelGGL(pgemm_x6_kernel<3>, dim3(total_wgs), dim3(256), 0, s, jobs_dev, wg_prefix_dev, njobs, slab);
+  }
   else
     hipLaunchKernelGGL(pgemm_kernel, dim3(total_wgs), dim3(256), 0, s, jobs_dev, wg_prefix_dev, njobs, slab);
   hipLaunchKernelGGL(pgemm_reduce_kernel, dim3((total_red + 255) / 256), dim3(256), 0, s, jobs_dev,

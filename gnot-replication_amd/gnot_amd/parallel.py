@@ -110,9 +110,16 @@ class PointShardComm:
                 t = self._view(buf, count)
                 with self._on(stream):
                     if self.stage:
+                        # host staging (gloo, tests): the whole device first, then blocking copies.  Under
+                        # ExternalStream(0) (a rank whose current stream is the null stream) .cpu() did NOT
+                        # wait for the engine's kernels: the 2-rank sharded 70k test read state buffers before
+                        # the state kernels ended (NaN forward at the first step, wrong gradients later;
+                        # r04sf, r05c-f)
+                        torch.cuda.synchronize(t.device)
                         h = t.cpu()
                         dist.all_reduce(h, group=self.group)
                         t.copy_(h)
+                        torch.cuda.synchronize(t.device)
                     else:
                         dist.all_reduce(t, group=self.group)
             return 0
@@ -129,9 +136,11 @@ class PointShardComm:
                 s = self._view(send, sum(sc)) if sum(sc) else torch.empty(0, device=dev)
                 r = self._view(recv, sum(rc)) if sum(rc) else torch.empty(0, device=dev)
                 if self.stage:
+                    torch.cuda.synchronize(dev)
                     hr = torch.empty(sum(rc), dtype=torch.float32)
                     dist.all_to_all_single(hr, s.cpu(), rc, sc, group=self.group)
                     r.copy_(hr)
+                    torch.cuda.synchronize(dev)
                 else:
                     dist.all_to_all_single(r, s, rc, sc, group=self.group)
             return 0

@@ -54,19 +54,20 @@ def rel(a, b):
 
 def check_parity(out, grads, fx, rtol=RTOL, slack=SLACK):
     errs = []
+    # every comparison is written `not (err <= bound)`: a NaN error (a non-finite output or gradient) fails
     e_out = rel(out, fx["out"])
-    if e_out > rtol:
+    if not e_out <= rtol:
         errs.append(f"output rel err {e_out:.3e} > {rtol}")
     if grads is not None:
         keys = sorted(fx["grads"])
         g = np.concatenate([np.ravel(grads[k]) for k in keys])
         r = np.concatenate([np.ravel(fx["grads"][k]) for k in keys])
         e_all = rel(g, r)
-        if e_all > rtol:
+        if not e_all <= rtol:
             errs.append(f"all-grad rel err {e_all:.3e} > {rtol}")
         for k in keys:
             d = float(np.linalg.norm(np.asarray(grads[k], np.float64) - fx["grads"][k]))
             lim = rtol * float(np.linalg.norm(fx["grads"][k])) + slack * fx["e32"].get(k, 0.0)
-            if d > lim:
+            if not d <= lim:
                 errs.append(f"{k}: |err| {d:.3e} > {lim:.3e}")
     return errs

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 import torch
 
-from test_gpu_configs import CFG_3D
+from test_gpu_configs import CFG_3D, CFG_CFG2
 from test_gpu_parity import _random_case, build_model, run_packed
 
 pytestmark = pytest.mark.gpu
@@ -40,6 +40,37 @@ def test_bf16_mode_within_1e2_of_fp64_reference(n_attn_layers):
     out32b, g32b = run_packed(m, fx, G)
     assert np.array_equal(out32b, out32)
     assert all(np.array_equal(g32b[k], g32[k]) for k in keys)
+
+
+def _bf16_vs_oracle(fx, G):
+    """(e_out, e_grad) of the bf16 mode vs the float64 oracle, after checking that the mode changes the
+    arithmetic and that switching back restores the fp32 bits"""
+    m = build_model(fx["params"], fx["cfg"])
+    out32, g32 = run_packed(m, fx, G)
+    m.set_precision("bf16")
+    m.zero_grad(set_to_none=True)
+    out16, g16 = run_packed(m, fx, G)
+    keys = list(fx["grads"].keys())
+    cat = lambda g: np.concatenate([g[k].ravel() for k in keys])
+    assert _rel(out16, out32) > 1e-6 and _rel(cat(g16), cat(g32)) > 1e-6
+    m.set_precision("fp32")
+    m.zero_grad(set_to_none=True)
+    out32b, g32b = run_packed(m, fx, G)
+    assert np.array_equal(out32b, out32) and all(np.array_equal(g32b[k], g32[k]) for k in keys)
+    return _rel(out16, fx["out"]), _rel(cat(g16), cat(fx["grads"]))
+
+
+@pytest.mark.timeout(300)
+def test_bf16_mode_configs1_exact_shape():
+    """configs[1] ("fp32 and bf16") in the bf16 mode at bench.py --workload cfg2's shape:
+    d = 128, 4 experts, 8 heads, 4 blocks, two 805-point input functions, one 10,000-point mesh.  At d <= 192
+    the mode runs chain.hip (k-major one-piece images, forward AND backward-data), linear.hip (output-major
+    one-piece projections) and the 128-tile weight gradients on one RNE bf16 piece per operand, fp32
+    accumulation; the attention contractions stay fp32 (as at d = 256).  north_star's 1e-2 vs float64."""
+    fx, G = _random_case(9, CFG_CFG2, [10000], [[805], [805]])
+    e_out, e_grad = _bf16_vs_oracle(fx, G)
+    print(f"\nconfigs[1] bf16 mode: output {e_out:.2e}, gradients {e_grad:.2e}")
+    assert e_out < 1e-2 and e_grad < 1e-2, (e_out, e_grad)
 
 
 def test_set_precision_rejects_unknown_dtype():

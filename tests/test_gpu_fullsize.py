@@ -3,7 +3,7 @@ points) -- far past what the float64 oracle can run, so checked through size-ind
 finite outputs and gradients, bitwise-repeatable steps (deterministic reductions), an inference forward
 (no saves) bitwise equal to the training forward, and a RelL2 loss that decreases over a few AdamW steps
 on a fixed target (main.py:50-103).  Both arithmetics: fp32 (bf16x6) and the bf16 mode, each in its
-default soft-MoE form (the expert grid; fused combine in the backward, and in the bf16 forward)."""
+default soft-MoE form (the expert grid and the moe_combine pass; bf16 mode: bf16 stage rows and moe_combine_b16)."""
 import pytest
 import torch
 

@@ -13,11 +13,12 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _run(monkeypatch, walk, recompute, E, I, d=256, prec="fp32"):
+def _run(monkeypatch, walk, recompute, E, I, d=256, prec="fp32", fused="0"):
     from gnot_amd import GNOT
     monkeypatch.setenv("GNOT_MOE_WALK", walk)
-    # serial weight gradients: a small plan that forks them sums the expert grid's stage with the combine
-    # pass (engine.cpp moe_fused), and the grid run here must be the grid with its fused combine
+    # fused="1": the opt-in fused combine (GNOT_MOE_FUSED, engine.cpp moe_fused), which needs serial weight
+    # gradients; the default grid sums its stage with the moe_combine pass (bf16 mode: moe_combine_b16)
+    monkeypatch.setenv("GNOT_MOE_FUSED", fused)
     monkeypatch.setenv("GNOT_WGRAD_OVERLAP", "0")
     dev = torch.device("cuda")
     torch.manual_seed(17)
@@ -44,11 +45,14 @@ def test_walk_form_bitwise_equals_expert_grid(monkeypatch, E, I, prec):
     o0, g0 = _run(monkeypatch, "0", False, E, I, prec=prec)
     o1, g1 = _run(monkeypatch, "1", False, E, I, prec=prec)
     o2, g2 = _run(monkeypatch, "1", True, E, I, prec=prec)
+    o3, g3 = _run(monkeypatch, "0", False, E, I, prec=prec, fused="1")   # the opt-in fused combine
     assert torch.isfinite(o0).all()
     diff = lambda a, b: f"max |diff| {float((a - b).abs().max()):.3e} of max {float(a.abs().max()):.3e}"
     assert torch.equal(o0, o1), "walk output: " + diff(o0, o1)
     assert torch.equal(o0, o2), "walk + recompute output: " + diff(o0, o2)
-    for k, (a, b, c) in enumerate(zip(g0, g1, g2)):
+    assert torch.equal(o0, o3), "fused combine output: " + diff(o0, o3)
+    for k, (a, b, c, f) in enumerate(zip(g0, g1, g2, g3)):
         assert torch.equal(a, b), f"parameter {k}: walk differs from the expert grid, " + diff(a, b)
         assert torch.equal(a, c), f"parameter {k}: walk + recompute differs from the expert grid, " + diff(a, c)
+        assert torch.equal(a, f), f"parameter {k}: the fused combine differs from the combine pass, " + diff(a, f)
 

@@ -86,3 +86,71 @@ def test_padded_256_width_bf16_mode(name):
     e_out, e_grad = rel(out16, fx["out"]), rel(cat(g16), cat(fx["grads"]))
     assert e_out < 1e-2 and e_grad < 1e-2, (e_out, e_grad)
     assert rel(out16, out32) > 1e-6
+
+
+# wide input / output widths at d > 256: the first and last Linears of the chains run the projection kernel
+# at the plan's full padded width (engine.cpp kt_of: one tile, or every tile of the hidden width)
+CASES["d320_wide_io"] = dict(input_dim=150, theta_dim=60, input_func_dim=200, out_dim=200, n_attn_layers=1, d=320,
+                             n_mlp_num_layers=2, n_expert=2, n_head=10, n_input_functions=1)
+
+
+def test_wide_io_widths_above_256():
+    """input_dim + theta_dim = 210, input_func_dim = 200 and out_dim = 200 beside a d = 320 hidden width
+    (chainw.hip: every first / last Linear at the 320-wide projection instantiation) vs the oracle."""
+    fx, G = _case("d320_wide_io")
+    m = build_model(fx["params"], fx["cfg"])
+    out, grads = run_packed(m, fx, G)
+    errs = check_parity(out, grads, fx)
+    assert not errs, errs
+
+
+@pytest.mark.parametrize("name", ["d100_h5", "d208_h13", "d288_h18"])
+def test_padded_width_pad_columns_stay_zero_across_steps(name):
+    """Padded widths keep their pad columns at exact zero only because the workspace is cleared at bind
+    and no kernel writes a non-zero pad value.  Three steps on one bound plan: the
+    first and third on the case's inputs, the second on other inputs (other values in every reused
+    buffer); the third step's output and gradients must be bitwise the first's."""
+    import numpy as np
+    import torch
+    fx, G = _case(name)
+    m = build_model(fx["params"], fx["cfg"])
+    out1, g1 = run_packed(m, fx, G)
+    rng = np.random.default_rng(99)
+    fx2 = dict(fx, x=rng.random(fx["x"].shape) * 3 - 1, theta=rng.random(fx["theta"].shape) * 5,
+               fns=[rng.random(f.shape) * 4 - 2 for f in fx["fns"]])
+    run_packed(m, fx2, rng.standard_normal(G.shape) * 10)
+    out3, g3 = run_packed(m, fx, G)
+    assert np.array_equal(out1, out3)
+    assert all(np.array_equal(g1[k], g3[k]) for k in g1), [k for k in g1 if not np.array_equal(g1[k], g3[k])]
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("name", ["d16_h4", "d96_h8", "d100_h5", "d144_h4", "d176_h4", "d192_h6"])
+def test_width_bf16_mode(name):
+    """The bf16 arithmetic mode at d <= 192 (chain.hip / linear.hip / the 128-tile weight gradients on one
+    RNE bf16 piece per operand), padded widths included: north_star's 1e-2 norm-wise vs the fp64 oracle, and
+    really another arithmetic than the fp32 path."""
+    import numpy as np
+    fx, G = _case(name)
+    m = build_model(fx["params"], fx["cfg"])
+    out32, g32 = run_packed(m, fx, G)
+    m.set_precision("bf16")
+    out16, g16 = run_packed(m, fx, G)
+    keys = list(fx["grads"].keys())
+    cat = lambda g: np.concatenate([g[k].ravel() for k in keys])
+    rel = lambda a, b: float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+    e_out, e_grad = rel(out16, fx["out"]), rel(cat(g16), cat(fx["grads"]))
+    assert e_out < 1e-2 and e_grad < 1e-2, (e_out, e_grad)
+    assert rel(out16, out32) > 1e-6
+
+
+def test_bf16_mode_above_256_runs_the_fp32_path():
+    """Above d = 256 (chainw.hip, fp32-MFMA projections) the bf16 mode has no one-piece kernels: the results
+    are the fp32 path's, bit for bit."""
+    import numpy as np
+    fx, G = _case("d320_h10")
+    m = build_model(fx["params"], fx["cfg"])
+    out32, g32 = run_packed(m, fx, G)
+    m.set_precision("bf16")
+    out16, g16 = run_packed(m, fx, G)
+    assert np.array_equal(out16, out32) and all(np.array_equal(g16[k], g32[k]) for k in g32)
