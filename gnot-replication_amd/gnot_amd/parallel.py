@@ -99,10 +99,14 @@ class PointShardComm:
         return self.ws[off: off + 4 * n].view(torch.float32)
 
     def _on(self, stream):
-        """torch stream context for the engine's HIP stream handle (no-op for host buffers)."""
+        """torch stream context for the engine's HIP stream handle (no-op for host buffers).  The null
+        stream (handle 0: a caller whose current stream is torch's default stream) is torch's own default
+        stream object, not ExternalStream(0) (tests/test_gpu_shard.py::test_comm_stream_orders_after_kernels)."""
         if self.ws is None or not self.ws.is_cuda:
             return contextlib.nullcontext()
-        return torch.cuda.stream(torch.cuda.ExternalStream(int(stream or 0), device=self.ws.device))
+        if not stream:
+            return torch.cuda.stream(torch.cuda.default_stream(self.ws.device))
+        return torch.cuda.stream(torch.cuda.ExternalStream(int(stream), device=self.ws.device))
 
     def _allreduce(self, user, buf, count, stream):
         try:

@@ -263,3 +263,43 @@ def test_point_sharded_input_grads():
         p.join(timeout=60)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert not errs, errs
+
+
+@pytest.mark.parametrize("which", ["default", "external0", "side"])
+def test_comm_stream_orders_after_kernels(which):
+    """PointShardComm runs its collectives under the stream the engine hands it (parallel.PointShardComm._on).
+    Whatever that handle is -- 0 for a caller on torch's default (null) stream, or a side stream -- a copy
+    issued under it must see the result of the long kernel queued just before on that stream.  "external0"
+    is the round-4 form (ExternalStream(0)), kept here as the record of what the test checks; the product
+    path maps handle 0 to torch.cuda.default_stream."""
+    dev = torch.device("cuda", 0)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream(dev) if which == "side" else torch.cuda.default_stream(dev)
+    a = torch.randn(4096, 4096, device=dev)
+    ok = True
+    for _ in range(3):
+        with torch.cuda.stream(s):
+            t = torch.zeros(1, device=dev)
+            b = a
+            for _ in range(8):
+                b = b @ a / 64.0          # ~10 ms of queued work before the last write
+            t.fill_(1.0)
+        if which == "external0":
+            ctx = torch.cuda.stream(torch.cuda.ExternalStream(0, device=dev))
+        elif which == "default":
+            from gnot_amd import parallel as par
+            c = par.PointShardComm.__new__(par.PointShardComm)
+            c.ws = t
+            ctx = c._on(0)
+        else:
+            from gnot_amd import parallel as par
+            c = par.PointShardComm.__new__(par.PointShardComm)
+            c.ws = t
+            ctx = c._on(s.cuda_stream)
+        with ctx:
+            h = t.cpu()
+        ok = ok and float(h[0]) == 1.0
+        torch.cuda.synchronize()
+    if which == "external0" and not ok:
+        pytest.xfail("ExternalStream(0) does not order after the null stream's kernels on this stack")
+    assert ok
