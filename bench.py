@@ -285,9 +285,9 @@ def main():
     ap.add_argument("--breakdown", action="store_true", help="print per-kernel-class device time to stderr")
     ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32",
                     help="fp32: the reference's arithmetic (bf16x6-exact MFMA); bf16: configs[2]'s bf16 training "
-                         "(one RNE bf16 operand per MFMA in the d=256 chains / projections / weight gradients, "
-                         "fp32 accumulation; the soft-MoE chains keep their saves, dZ and Linear inputs in bf16; "
-                         "north_star's 1e-2 bar, tests/test_gpu_bf16.py)")
+                         "(one RNE bf16 operand per MFMA in the chains / projections / weight gradients up to d=256, "
+                         "fp32 accumulation; at d=256 the soft-MoE chains keep their saves, dZ and Linear inputs in "
+                         "bf16; north_star's 1e-2 bar, tests/test_gpu_bf16.py)")
     ap.add_argument("--fp32-only", action="store_true",
                     help="skip the companion bf16-mode measurement of the default fp32 run (configs[2], N=1)")
     ap.add_argument("--recompute", choices=["auto", "on", "off"], default="auto",
@@ -446,11 +446,12 @@ def main():
                   "wgrad_b16": "pgemm_b16_kernel+pgemm_reduce_kernel (soft-MoE weight gradients on bf16 rows, "
                                "LDS-DMA + ds_read_b64_tr_b16, bf16 MFMA)"}
                  if d256 else
-                 {"moe_fwd": "chain_fwd_kernel (fused MoE expert chains, forward, bf16x6 MFMA)",
-                  "moe_bwd": "chain_bwd_kernel (fused MoE expert chains, backward, fp32 MFMA)",
-                  "wgrad": "pgemm_x6_kernel+pgemm_reduce_kernel (weight gradients, bf16x6 MFMA)"})
+                 {"moe_fwd": f"chain_fwd_kernel (fused MoE expert chains, forward, {form} MFMA)",
+                  "moe_bwd": "chain_bwd_kernel (fused MoE expert chains, backward, "
+                             + ("fp32" if dtype == "fp32" else "bf16") + " MFMA)",
+                  "wgrad": f"pgemm_x6_kernel+pgemm_reduce_kernel (weight gradients, {form} MFMA)"})
         rk = M["rkind"]
-        if dtype == "bf16" and d256:
+        if dtype == "bf16" and m["n_attn_hidden_dim"] <= 256:
             pipe, pipe_peak = "bf16 MFMA (one product per block)", BF16_MFMA_PEAK_TFLOPS
         elif not d256 and rk == "moe_bwd":
             pipe, pipe_peak = "fp32 MFMA", FP32_MFMA_PEAK_TFLOPS

@@ -43,7 +43,7 @@ class Engine:
         self.comm = None           # parallel.PointShardComm when points are sharded over ranks
         self.grad_comm = None      # parallel.PointShardComm: gradients summed over ranks inside the backward
         self.moe_recompute = False # re-run each MoE call's expert forward in the backward (memory option)
-        self.bf16 = False          # bf16 arithmetic mode of the d = 256 MFMA kernels (gnot_plan_set_precision)
+        self.bf16 = False          # bf16 arithmetic mode of the MFMA kernels up to d = 256 (gnot_plan_set_precision)
         self.input_grads = False   # also differentiate x, theta, input functions (gnot_plan_set_input_grads)
         self.fwd_token = 0
 

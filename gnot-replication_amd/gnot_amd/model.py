@@ -177,11 +177,12 @@ class GNOT(nn.Module):
 
     def set_precision(self, dtype):
         """'fp32' (default: the reference's fp32 arithmetic, bf16x6-exact on the MFMA) or 'bf16' (BASELINE
-        configs[2]'s bf16 training: ONE round-to-nearest bf16 operand piece per MFMA in the d = 256 MLP
-        chains, attention projections and weight gradients, fp32 accumulation; the soft-MoE expert chains
-        keep their training saves (gelu'(h), expert outputs), dZ and Linear inputs in bf16, which the MoE
-        weight gradients read directly; parameters, the other activations and the attention contractions
-        stay fp32).  Other hidden widths are unaffected."""
+        configs[2]'s bf16 training, configs[1]'s "fp32 and bf16": ONE round-to-nearest bf16 operand piece
+        per MFMA in the MLP chains, attention projections and weight gradients of every hidden width up to
+        256, fp32 accumulation; at d = 256 the soft-MoE expert chains also keep their training saves
+        (gelu'(h), expert outputs), dZ and Linear inputs in bf16, which the MoE weight gradients read
+        directly; parameters, the other activations and the attention contractions stay fp32).  Above
+        d = 256 (the layer-wise chains) the fp32 path runs in either mode."""
         d = str(dtype).replace("torch.", "")
         if d in ("bf16", "bfloat16"):
             self._bf16 = True

@@ -90,14 +90,15 @@ int gnot_plan_set_batch(gnot_plan* plan, int B, const int64_t* x_off, const int6
  * memory option of this library; torch.utils.checkpoint is the analogue). */
 int gnot_plan_set_moe_recompute(gnot_plan* plan, int on);
 
-/* Arithmetic mode of the d = 256 MFMA kernels (MLP chains, attention projections, weight gradients):
- * bf16 == 0 (default) runs them as bf16x6 -- three exact bf16 pieces per fp32 operand, six products,
- * fp32-level results (north_star's 1e-4 bar); bf16 != 0 runs ONE round-to-nearest-even bf16 piece per
- * operand with fp32 accumulation (BASELINE configs[2]'s bf16 training; north_star's 1e-2 bar), and
- * the soft-MoE expert chains keep their training saves, dZ and Linear inputs as bf16 rows (the MoE
- * weight gradients read them directly).  Parameters, the other activations, states, gradients and the
- * attention contractions stay fp32 either way; other widths are unaffected.  Changing it invalidates
- * the batch (set_batch + bind again). */
+/* Arithmetic mode of the MFMA kernels up to hidden width 256 (MLP chains, attention projections, weight
+ * gradients): bf16 == 0 (default) runs them as bf16x6 -- three exact bf16 pieces per fp32 operand, six
+ * products, fp32-level results (north_star's 1e-4 bar; the d <= 192 chain backward-data on exact fp32
+ * MFMA); bf16 != 0 runs ONE round-to-nearest-even bf16 piece per operand with fp32 accumulation
+ * (BASELINE configs[2]'s bf16 training, configs[1]'s "fp32 and bf16"; north_star's 1e-2 bar), and at
+ * d = 256 the soft-MoE expert chains keep their training saves, dZ and Linear inputs as bf16 rows (the
+ * MoE weight gradients read them directly).  Parameters, the other activations, states, gradients and
+ * the attention contractions stay fp32 either way; above d = 256 the mode changes nothing.  Changing it
+ * invalidates the batch (set_batch + bind again). */
 int gnot_plan_set_precision(gnot_plan* plan, int bf16);
 
 /* Input gradients (off by default).  The reference's autograd also differentiates w.r.t. x, theta and
