@@ -139,16 +139,18 @@ __global__ void __launch_bounds__(64 * kChainWaves) chain_bwd_kernel(ChainArgs a
   const ChainLayer* L = a.layers + e * nl;
   const float* save = a.save + e * a.save_chain_stride;
   float* dz = a.dz ? a.dz + e * a.dz_chain_stride : nullptr;
-  constexpr bool B1 = NP == 1;
-  __shared__ __attribute__((aligned(16))) float4 wlds[B1 ? 2 * x6_buf_f4(D) : 2 * kChunkF4];
+  // k-major NP-piece images of W^T on the bf16 MFMA (bf16 mode, and bf16x6 in the fp32 mode unless built
+  // with GNOT_CHAIN_BWD_FP32), or fp32 fragment images on the exact fp32 MFMA
+  constexpr bool BX = NP == 1 || kChainBwdX6;
+  __shared__ __attribute__((aligned(16))) float4 wlds[BX ? 2 * x6_buf_f4(D) : 2 * kChunkF4];
   int cnt = 0;
-  // chunk of a KT-deep, OT-wide transposed image: fp32 fragment tiles, or one-piece k-major blocks
-  auto cf4 = [](int KT, int OT) { return B1 ? x6_chunk_f4<D, 1>(KT, OT) : chunk_f4(KT, OT); };
+  // chunk of a KT-deep, OT-wide transposed image: fp32 fragment tiles, or NP-piece k-major blocks
+  auto cf4 = [](int KT, int OT) { return BX ? x6_chunk_f4<D, NP>(KT, OT) : chunk_f4(KT, OT); };
   // acc += W^T in over the KT-deep image Wg (the weight stream of the pipe of this arithmetic)
   auto mm = [&](auto KTc, auto OTc, const float4* Wg, const float4* nW, int nf4, const float (&in)[decltype(KTc)::value][4],
                 f32x4 (&acc)[decltype(OTc)::value], auto hook) __attribute__((always_inline)) {
     constexpr int KT = decltype(KTc)::value, OT = decltype(OTc)::value;
-    if constexpr (B1) mm_tiles_pipe_x6<D, KT, OT, 1>(Wg, nW, nf4, wlds, cnt, in, acc, kChainWaves, wave, lane, hook);
+    if constexpr (BX) mm_tiles_pipe_x6<D, KT, OT, NP>(Wg, nW, nf4, wlds, cnt, in, acc, kChainWaves, wave, lane, hook);
     else mm_tiles_pipe<KT, OT>(Wg, nW, nf4, wlds, cnt, in, acc, kChainWaves, wave, lane, hook);
   };
   using IOTL = std::integral_constant<int, OTL>;

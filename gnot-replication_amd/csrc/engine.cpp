@@ -63,6 +63,7 @@ struct WgradGroup {
   size_t slab_floats = 0;
   bool x6 = false;                   // plain weight-gradient jobs: the bf16x6 MFMA kernel
   bool wide = false;                 // ... on the 256 x 256-tile kernel (d = 256: one workgroup per job split)
+  int tw = 256;                      // wide geometry's output edge: 256, or 128 (d <= 128, jobs within 128 x 128)
   bool b16 = false;                  // bf16-storage jobs (bf16 mode soft-MoE): pgemm_b16_kernel, wide geometry
   std::vector<int> lins;             // weight-gradient groups: the canonical Linears whose (dW, db) they write
   int state_pts = 0, state_nw = 0;
@@ -177,6 +178,14 @@ struct gnot_plan {
   bool stage_used[kStageSlots] = {};
   int stage_next = 0;
   std::map<const float*, hipEvent_t> readers;
+  // forked weight-gradient groups whose side-stream launch waits until the caller's stream has enqueued
+  // its next kernel (run_wgrad_side / flush_deferred)
+  struct DeferredWgrad {
+    const WgradGroup* G;
+    std::vector<const float*> reads;
+    hipEvent_t fork;
+  };
+  std::vector<DeferredWgrad> deferred;
   int4* d_qchunks = nullptr;
   int* d_qchunk_off = nullptr;
   std::vector<int4*> d_fchunks;
@@ -503,8 +512,10 @@ static void plan_images(gnot_plan* p) {
       Img f = cw ? new_img(OTp, KTp) : new_img_x6(OTp, KTp, c2 ? c2np : b1 ? 1 : 3);
       const size_t bo = new_bias(16 * OTp);
       job(li, f, 0, 0, OTp, KTp, 0, (long)bo, cw ? 0 : c2 ? c2x6 : b1 ? 4 : 1);
-      Img t = c2 ? new_img_x6(KTp, OTp, c2np) : b1 ? new_img_x6(KTp, OTp, 1) : new_img(KTp, OTp);   // backward-data
-      job(li, t, 0, 0, KTp, OTp, 1, -1, c2 ? c2x6 : b1 ? 4 : 0);
+      // backward-data image: d <= 192 k-major x6 (kChainBwdX6) or one-piece (bf16 mode), else fp32 tiles
+      const bool tx6 = !c2 && !cw && (b1 || kChainBwdX6);
+      Img t = c2 ? new_img_x6(KTp, OTp, c2np) : tx6 ? new_img_x6(KTp, OTp, b1 ? 1 : 3) : new_img(KTp, OTp);
+      job(li, t, 0, 0, KTp, OTp, 1, -1, c2 ? c2x6 : tx6 ? (b1 ? 4 : 1) : 0);
       p->fwd_img[li] = f;
       p->T_img[li] = t;
       p->fwd_bias[li] = bo;
@@ -582,6 +593,15 @@ static void plan_images(gnot_plan* p) {
 }
 
 // ====================================================================== point-reduction GEMM groups
+static bool wgrad128_on() {
+  const char* e = std::getenv("GNOT_WGRAD128");
+  return !(e && e[0] == '0');
+}
+// split-K target of the 128-wide kernel (GNOT_WGRAD128_WGS overrides: A/B runs)
+static long wide128_wgs() {
+  const char* e = std::getenv("GNOT_WGRAD128_WGS");
+  return e ? std::max(1L, std::atol(e)) : 128;
+}
 static void finish_group(gnot_plan* p, WgradGroup& G) {
   G.x6 = true;
   for (const auto& J : G.jobs)
@@ -596,8 +616,17 @@ static void finish_group(gnot_plan* p, WgradGroup& G) {
   G.wide = G.x6 && p->D == 256 && !G.jobs.empty();
   for (const auto& J : G.jobs)
     if (J.out > 256 || J.in > 256) G.wide = false;
+  G.tw = 256;
+  // d <= 128 (configs[1]): the wide kernel's design at a 128 x 128 output (4 waves, staging interleaved with
+  // the MFMAs, raw rows by LDS-DMA) instead of the 128-tile kernel (GNOT_WGRAD128=0 keeps that one)
+  if (G.x6 && !G.wide && p->D <= 128 && !G.jobs.empty() && wgrad128_on()) {
+    bool fits = true;
+    for (const auto& J : G.jobs)
+      if (J.out > 128 || J.in > 128) fits = false;
+    if (fits) { G.wide = true; G.tw = 128; }
+  }
   if (G.b16) G.wide = true;          // the bf16-storage kernel has the wide kernel's geometry
-  const long target = G.wide ? wide_wgs : G.x6 ? x6_wgs : kTargetWGs;
+  const long target = G.wide ? (G.tw == 128 ? wide128_wgs() : wide_wgs) : G.x6 ? x6_wgs : kTargetWGs;
   long tiles = 0;
   for (auto& J : G.jobs) {
     J.tiles_o = (J.out + kPTile - 1) / kPTile;
@@ -1577,7 +1606,14 @@ hipEvent_t next_event(gnot_plan* p) {
 }
 
 // before the main stream overwrites `buf`, wait for the side-stream group that last read it
+int flush_deferred(Ctx& c);
 int guard_write(Ctx& c, const float* buf) {
+  for (const auto& d : c.p->deferred)         // a deferred group reads buf: launch it (and register) first
+    if (std::find(d.reads.begin(), d.reads.end(), buf) != d.reads.end()) {
+      const int rc = flush_deferred(c);
+      if (rc != GNOT_OK) return rc;
+      break;
+    }
   auto it = c.p->readers.find(buf);
   if (it != c.p->readers.end()) {
     GNOT_CK(hipStreamWaitEvent(c.s, it->second, 0));
@@ -1599,7 +1635,7 @@ int launch_group(gnot_plan* p, const WgradGroup& G, float* slab, hipStream_t s) 
                              slab, s));
   else
     GNOT_CK(launch_wgrad(G.d_jobs, G.d_wg_prefix, (int)G.jobs.size(), G.total_wgs, G.d_red_prefix, G.total_red, slab,
-                         s, G.x6, G.wide, p->npk()));
+                         s, G.x6, G.wide, p->npk(), G.tw));
   return GNOT_OK;
 }
 
@@ -1653,18 +1689,34 @@ int run_wgrad_side(Ctx& c, const WgradGroup& G, std::initializer_list<const floa
     }
     return GNOT_OK;
   }
+  // forked: the side stream waits for what the caller's stream has issued so far (the fork event is
+  // recorded now), but its launches are captured only after the caller's NEXT kernel (flush_deferred).  A
+  // captured graph keeps a node's first-captured child on the node's own hardware queue; with the side
+  // launch captured first, the main chain hopped to another queue at every fork, ~10 us of cross-queue
+  // wait each (configs[1] trace, profiles/r05m_*: 8 MoE calls x 2 forks per step)
   hipEvent_t fork = next_event(p);
   GNOT_CK(hipEventRecord(fork, c.s));
-  GNOT_CK(hipStreamWaitEvent(p->side, fork, 0));
-  {
-    // profiled as its own class: the bf16-row MoE weight gradients are HBM-bound, the others are not
-    ProfScope ps(c, G.b16 ? "wgrad_b16" : "wgrad", group_flops(G), p->side);
-    GNOT_RUN(launch_group(p, G, p->P_("slab_wgrad"), p->side));
+  p->deferred.push_back({&G, std::vector<const float*>(reads), fork});
+  return GNOT_OK;
+}
+
+// the deferred side-stream weight-gradient groups, in order; `c` is the capture-origin stream's context
+int flush_deferred(Ctx& c) {
+  gnot_plan* p = c.p;
+  std::vector<gnot_plan::DeferredWgrad> pend;
+  pend.swap(p->deferred);
+  for (const auto& d : pend) {
+    GNOT_CK(hipStreamWaitEvent(p->side, d.fork, 0));
+    {
+      // profiled as its own class: the bf16-row MoE weight gradients are HBM-bound, the others are not
+      ProfScope ps(c, d.G->b16 ? "wgrad_b16" : "wgrad", group_flops(*d.G), p->side);
+      GNOT_RUN(launch_group(p, *d.G, p->P_("slab_wgrad"), p->side));
+    }
+    hipEvent_t done = next_event(p);
+    GNOT_CK(hipEventRecord(done, p->side));
+    for (const float* r : d.reads) p->readers[r] = done;
+    if (p->grad_comm_on) GNOT_RUN(grad_allreduce(p, *d.G, done));
   }
-  hipEvent_t done = next_event(p);
-  GNOT_CK(hipEventRecord(done, p->side));
-  for (const float* r : reads) p->readers[r] = done;
-  if (p->grad_comm_on) GNOT_RUN(grad_allreduce(p, G, done));
   return GNOT_OK;
 }
 
@@ -1961,6 +2013,7 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
   float* dquery = p->P_("dquery");
   float* stage = p->moe_walk ? nullptr : p->P_("stage");
   p->readers.clear();
+  p->deferred.clear();
   if (p->grad_comm_on) {                   // the comm stream joins here (a first-level fork of the caller's)
     if (!p->comm_stream) GNOT_CK(hipStreamCreateWithFlags(&p->comm_stream, hipStreamNonBlocking));
     hipEvent_t fork = next_event(p);
@@ -1981,6 +2034,7 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
       ProfScope ps(cc, prof, 2.0 * a.nchains * rows * NL * (double)D * D);
       GNOT_CK(launch_chain_bwd(cw_scratch(p, a, cc.s), cc.s));
     }
+    if (cc.s == c.s) GNOT_RUN(flush_deferred(cc));   // earlier groups' side launches after this kernel
     // the weight gradients read the saved pre-activations too: a recomputed (shared) save buffer
     // must not be overwritten by the next MoE's recompute before they finish.  That guard is the
     // readers map, which only run_wgrad_side from the capture-origin stream registers (side2 runs its
@@ -2039,6 +2093,7 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
       }
       GNOT_RUN(chain_bwd(a, m1 ? p->k_m1(l) : p->k_m2(l), P, m1 ? p->wg_m1[l] : p->wg_m2[l], "moe_bwd"));
       if (!walk && !moe_fused(p, true)) GNOT_CK(launch_moe_pass(p, nullptr, stage, dsum, c.s));
+      GNOT_RUN(flush_deferred(c));            // the chain's weight gradients: side launch after the pass
       // m2: self attention (model.py:133) ; m1: cross attention (model.py:127)
       GNOT_RUN(attn_backward(c, l, m1));
     }
@@ -2099,6 +2154,7 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
     GNOT_CK(hipEventRecord(joinf, cf.s));
     GNOT_CK(hipStreamWaitEvent(c.s, joinf, 0));
   }
+  GNOT_RUN(flush_deferred(c));
   // join the side stream: every gradient is complete when the caller's stream moves on
   hipEvent_t join = next_event(p);
   GNOT_CK(hipEventRecord(join, p->side));

@@ -132,6 +132,13 @@ struct ChainArgs {
   // launch_moe_combine_b16
   int stage_b16 = 0;
 };
+// d <= 192 chain backward-data in the fp32 mode: bf16x6 on k-major 3-piece images of W^T (pack x6 = 1), as
+// the forward; -DGNOT_CHAIN_BWD_FP32 builds the round-1..4 form (exact fp32 MFMA on fp32 fragment images)
+#ifdef GNOT_CHAIN_BWD_FP32
+constexpr bool kChainBwdX6 = false;
+#else
+constexpr bool kChainBwdX6 = true;
+#endif
 // walk or per-expert grid for a MoE call of P points (env GNOT_MOE_WALK = 0 / 1 forces, read per call)
 bool chain2_walk_choice(long P, int E);
 // d > 256: chains one Linear at a time (linear.hip + elementwise passes, chainw.hip)
@@ -165,9 +172,10 @@ struct WgradJob {
 // x6: plain weight-gradient jobs only (no w, state_dh, diag_only) on the bf16x6 MFMA kernel
 // wide: the same on the 256 x 256-tile kernel (out, in <= 256; ONE workgroup per (job, split), so
 //       wg_prefix counts splits only)
+// tw: the wide kernel's output edge, 256 (d = 256) or 128 (d <= 128: every job within 128 x 128)
 hipError_t launch_wgrad(const WgradJob* jobs_dev, const int* wg_prefix_dev, int njobs, int total_wgs,
                         const int* red_prefix_dev, int total_red, float* slab, hipStream_t s, bool x6 = false,
-                        bool wide = false, int np = 3);   // np: the wide kernel's operand pieces (1 = bf16 mode)
+                        bool wide = false, int np = 3, int tw = 256);   // np: operand pieces (1 = bf16 mode)
 // bf16-storage jobs (ChainArgs::b16s): dz and x point at bf16 pair-interleaved rows [P, 256] (x already
 // the Linear's input, no GELU), out = in = 256, one workgroup per (job, split) as the wide kernel
 hipError_t launch_wgrad_b16(const WgradJob* jobs_dev, const int* wg_prefix_dev, int njobs, int total_wgs,

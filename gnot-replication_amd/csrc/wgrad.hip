@@ -379,15 +379,21 @@ __global__ void __launch_bounds__(256) pgemm_x6_kernel(const WgradJob* __restric
 //            piece products each (smallest first), one accumulator per block.
 // Double-buffered fragment images: stage s+1 is split into the other buffer while stage s is multiplied.
 // Partials go to the same slab layout as pgemm_kernel (128-tiles).
+// TW = 128 (round 5): the same kernel at d <= 128 (configs[1]) with a 128 x 128 output per workgroup and 4
+// waves (one 64 x 64 quadrant each, 2 x 2 blocks), in place of the 128-tile kernel above, whose staging and
+// MFMAs run as separate phases on one wave per SIMD.
 constexpr int kWStage = 16;
-constexpr int kWThreads = 512;
-constexpr int kWPiece = 8 * 64;                  // u32x4 per (operand, piece) image
+constexpr int kWThreads = 512;                   // TW = 256; TW = 128: 256
+constexpr int w_threads(int tw) { return tw * 2; }
+constexpr int w_piece(int tw) { return tw / 32 * 64; }   // u32x4 per (operand, piece) image
 // one stage buffer: A pieces 0..NP-1 | B pieces 0..NP-1 (NP = 3: bf16x6, 1: bf16 mode)
-constexpr int w_buf(int np) { return 2 * np * kWPiece; }
+constexpr int w_buf(int np, int tw = 256) { return 2 * np * w_piece(tw); }
 constexpr int kWRawSlot = 2 * 2 * 64;            // u32x4 per wave-private raw slot: 2 operands x 2 KiB
 constexpr int kWRawSlots = 2;
-// LDS: two fragment buffers | 8 waves x 2 raw slots (96 + 64 = 160 KiB at NP = 3)
-constexpr size_t w_lds_bytes(int np) { return (2 * (size_t)w_buf(np) + 8 * kWRawSlots * kWRawSlot) * 16; }
+// LDS: two fragment buffers | waves x 2 raw slots (96 + 64 = 160 KiB at NP = 3, TW = 256; 48 + 32 at 128)
+constexpr size_t w_lds_bytes(int np, int tw = 256) {
+  return (2 * (size_t)w_buf(np, tw) + (size_t)(tw / 32) * kWRawSlots * kWRawSlot) * 16;
+}
 
 // one dword of a wave-private raw slot (inline asm: the compiler does not order it against the LDS-DMA
 // still in flight to the OTHER slot; the caller's counted vmcnt already retired this slot's DMA, and a
@@ -399,10 +405,15 @@ GNOT_DEV float lds_read_b32_off(unsigned addr) {
   return v;
 }
 
-template <int NP = 3>
-__global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __restrict__ jobs,
-                                                              const int* __restrict__ prefix, int njobs,
-                                                              float* __restrict__ slab) {
+template <int NP = 3, int TW = 256>
+__global__ void __launch_bounds__(w_threads(TW)) pgemm_x6w_kernel(const WgradJob* __restrict__ jobs,
+                                                                 const int* __restrict__ prefix, int njobs,
+                                                                 float* __restrict__ slab) {
+  constexpr int NW = TW / 32;            // waves
+  constexpr int FG = TW / 64;            // 64-feature groups of the raw-row DMA
+  constexpr int WC = NW / 2;             // waves along the columns
+  constexpr int RB = TW / 64;            // 32-row blocks per wave (columns: 2 blocks per wave)
+  constexpr int kWPiece = w_piece(TW);
   extern __shared__ __attribute__((aligned(16))) u32x4 wl[];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -413,20 +424,20 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
   const long pb = (long)split * chunk;
   const long pe = min((long)J.P, pb + chunk);
   const int nst = pe > pb ? (int)((pe - pb + kWStage - 1) / kWStage) : 0;
-  // staging role (the point half hh is wave-uniform: waves 0-3 / 4-7)
-  const int f = tid & 255, hh = tid >> 8;
+  // staging role (the point half hh is wave-uniform: waves 0 .. NW/2-1 / NW/2 ..)
+  const int f = tid & (TW - 1), hh = tid / TW;
   const bool fa = f < J.out, fb = f < J.in;
   const int sdst = (f >> 5) * 64 + (f & 31) + 32 * hh;
   // MFMA role
-  const int wr = wave >> 2, wc = wave & 3;
-  const int nrb = max(0, min(4, (J.out - 128 * wr + 31) / 32));
+  const int wr = wave / WC, wc = wave % WC;
+  const int nrb = max(0, min(RB, (J.out - 32 * RB * wr + 31) / 32));
   const int ncb = max(0, min(2, (J.in - 64 * wc + 31) / 32));
-  const bool full = nrb == 4 && ncb == 2;
+  const bool full = nrb == RB && ncb == 2;
   const bool gel = J.x_gelu != 0;
 
-  f32x16 acc[4][2];
+  f32x16 acc[RB][2];
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int a = 0; a < RB; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{};
   float dbacc = 0.f;
@@ -439,13 +450,13 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
   const rsrc_t rA = make_rsrc(J.dz + pb * J.lddz, (unsigned)(nsp * J.lddz * 4));
   const rsrc_t rB = make_rsrc(J.x + pb * J.ldx, (unsigned)(nsp * J.ldx * 4));
   // DMA lane role: instruction i of operand o brings points 4 i + (lane >> 4) of the wave's half, features
-  // 64 (wave & 3) + 4 (lane & 15) .. +3; in the slot, point k of the half is the 256-byte row k (64 floats)
-  const int fcol = 64 * (wave & 3) + 4 * (lane & 15);
+  // 64 (wave % FG) + 4 (lane & 15) .. +3; in the slot, point k of the half is the 256-byte row k (64 floats)
+  const int fcol = 64 * (wave % FG) + 4 * (lane & 15);
   const int dvA = ((lane >> 4) * (int)J.lddz + fcol) * 4, dvB = ((lane >> 4) * (int)J.ldx + fcol) * 4;
-  u32x4* const raw = wl + 2 * w_buf(NP) + wave * kWRawSlots * kWRawSlot;
+  u32x4* const raw = wl + 2 * w_buf(NP, TW) + wave * kWRawSlots * kWRawSlot;
   auto raw_dma = [&](int st) __attribute__((always_inline)) {
     u32x4* dst = raw + (st & 1) * kWRawSlot;
-    const unsigned p0 = (unsigned)(st * kWStage + 8 * (wave >> 2));
+    const unsigned p0 = (unsigned)(st * kWStage + 8 * (wave / FG));
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       dma16(rA, dst + i * 64, dvA, (int)((p0 + 4 * i) * (unsigned)J.lddz * 4u));
@@ -484,7 +495,7 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
     u32x4 pa[NP], pq[NP];
     split8_np<NP>(ra, pa);
     split8_np<NP>(vb, pq);
-    u32x4* base = wl + buf * w_buf(NP);
+    u32x4* base = wl + buf * w_buf(NP, TW);
 #pragma unroll
     for (int q = 0; q < NP; ++q) {
       base[q * kWPiece + sdst] = pa[q];
@@ -496,7 +507,7 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
     else stage_v(buf, std::false_type{});
   };
   auto compute = [&](int buf) {
-    const u32x4* A = wl + buf * w_buf(NP);
+    const u32x4* A = wl + buf * w_buf(NP, TW);
     const u32x4* Bm = A + NP * kWPiece;
     u32x4 bf[2][NP];
 #pragma unroll
@@ -504,11 +515,11 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
 #pragma unroll
       for (int q = 0; q < NP; ++q) bf[jb][q] = Bm[q * kWPiece + (wc * 2 + jb) * 64 + lane];
 #pragma unroll
-    for (int ib = 0; ib < 4; ++ib) {
+    for (int ib = 0; ib < RB; ++ib) {
       if (ib >= nrb) break;
       u32x4 af[NP];
 #pragma unroll
-      for (int q = 0; q < NP; ++q) af[q] = A[q * kWPiece + (wr * 4 + ib) * 64 + lane];
+      for (int q = 0; q < NP; ++q) af[q] = A[q * kWPiece + (wr * RB + ib) * 64 + lane];
       if (ncb > 0) mfma_np<NP>(af, bf[0], acc[ib][0]);
       if (ncb > 1) mfma_np<NP>(af, bf[1], acc[ib][1]);
     }
@@ -533,7 +544,7 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
     int buf = 0;
     // MASK: columns past out / in exist (the fa / fb selects); jobs with out = in = 256 skip them
     auto fused = [&](int b, auto GEL, auto MASK) {
-      const u32x4* A = wl + b * w_buf(NP);
+      const u32x4* A = wl + b * w_buf(NP, TW);
       const u32x4* Bm = A + NP * kWPiece;
       u32x4 bf[2][NP], af[2][NP], pa[NP], pq[NP];
 #pragma unroll
@@ -541,7 +552,7 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
 #pragma unroll
         for (int q = 0; q < NP; ++q) bf[jb][q] = Bm[q * kWPiece + (wc * 2 + jb) * 64 + lane];
 #pragma unroll
-      for (int q = 0; q < NP; ++q) af[0][q] = A[q * kWPiece + (wr * 4) * 64 + lane];
+      for (int q = 0; q < NP; ++q) af[0][q] = A[q * kWPiece + (wr * RB) * 64 + lane];
       float ra[8], vb[8];
       // after each six-MFMA group (one 32 x 32 block) one point's staging (mask, column sum, GELU; every
       // second point the split of the pair just finished); sched_barrier pins the order, so each wave
@@ -561,22 +572,26 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
           for (int q = 0; q < NP; ++q) asm volatile("" : "+v"(pa[q][k >> 1]), "+v"(pq[q][k >> 1]));
         }
       };
+      // 2 RB MFMA groups per stage and 8 points to stage: 8 / (2 RB) points after each group
+      constexpr int CPG = 8 / (2 * RB);
 #pragma unroll
-      for (int ib = 0; ib < 4; ++ib) {
-        if (ib + 1 < 4) {
+      for (int ib = 0; ib < RB; ++ib) {
+        if (ib + 1 < RB) {
 #pragma unroll
-          for (int q = 0; q < NP; ++q) af[(ib + 1) & 1][q] = A[q * kWPiece + (wr * 4 + ib + 1) * 64 + lane];
+          for (int q = 0; q < NP; ++q) af[(ib + 1) & 1][q] = A[q * kWPiece + (wr * RB + ib + 1) * 64 + lane];
         }
         mfma_np<NP>(af[ib & 1], bf[0], acc[ib][0]);
         __builtin_amdgcn_sched_barrier(0);
-        chunk(2 * ib);
+#pragma unroll
+        for (int k = 0; k < CPG; ++k) chunk(CPG * 2 * ib + k);
         __builtin_amdgcn_sched_barrier(0);
         mfma_np<NP>(af[ib & 1], bf[1], acc[ib][1]);
         __builtin_amdgcn_sched_barrier(0);
-        chunk(2 * ib + 1);
+#pragma unroll
+        for (int k = 0; k < CPG; ++k) chunk(CPG * (2 * ib + 1) + k);
         __builtin_amdgcn_sched_barrier(0);
       }
-      u32x4* base = wl + (b ^ 1) * w_buf(NP);
+      u32x4* base = wl + (b ^ 1) * w_buf(NP, TW);
 #pragma unroll
       for (int q = 0; q < NP; ++q) {
         base[q * kWPiece + sdst] = pa[q];
@@ -596,7 +611,7 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
       }
     };
     if (full) {
-      if (J.out >= 256 && J.in >= 256) {
+      if (J.out >= TW && J.in >= TW) {
         if (gel) run(std::true_type{}, std::false_type{});
         else run(std::false_type{}, std::false_type{});
       } else {
@@ -623,12 +638,12 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
   const int ntile = J.tiles_o * J.tiles_i;
   float* S0 = slab + J.slab_off + (long)split * ntile * (kTile * (kTile + 1));
 #pragma unroll
-  for (int ib = 0; ib < 4; ++ib)
+  for (int ib = 0; ib < RB; ++ib)
 #pragma unroll
     for (int jb = 0; jb < 2; ++jb)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = wr * 128 + ib * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int row = wr * 32 * RB + ib * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
         const int col = wc * 64 + jb * 32 + (lane & 31);
         if (row < J.out && col < J.in)
           S0[((row >> 7) * J.tiles_i + (col >> 7)) * (kTile * (kTile + 1)) + (row & 127) * (kTile + 1) + (col & 127)] =
@@ -640,10 +655,10 @@ __global__ void __launch_bounds__(kWThreads) pgemm_x6w_kernel(const WgradJob* __
     // interleaved loop ends without a barrier)
     float* red = reinterpret_cast<float*>(wl);
     __syncthreads();
-    red[hh * 256 + f] = dbacc;
+    red[hh * TW + f] = dbacc;
     __syncthreads();
-    if (tid < 256 && f < J.out)
-      S0[((f >> 7) * J.tiles_i) * (kTile * (kTile + 1)) + (f & 127) * (kTile + 1) + kTile] = red[f] + red[256 + f];
+    if (tid < TW && f < J.out)
+      S0[((f >> 7) * J.tiles_i) * (kTile * (kTile + 1)) + (f & 127) * (kTile + 1) + kTile] = red[f] + red[TW + f];
   }
 }
 
@@ -853,22 +868,22 @@ hipError_t launch_wgrad_b16(const WgradJob* jobs_dev, const int* wg_prefix_dev, 
 
 hipError_t launch_wgrad(const WgradJob* jobs_dev, const int* wg_prefix_dev, int njobs, int total_wgs,
                         const int* red_prefix_dev, int total_red, float* slab, hipStream_t s, bool x6, bool wide,
-                        int np) {
+                        int np, int tw) {
   if (njobs <= 0) return hipSuccess;
   if (wide) {
-    const size_t lds = w_lds_bytes(np);
-#define GNOT_X6W(NP_)                                                                                          \
-  if (np == NP_) {                                                                                             \
+    const size_t lds = w_lds_bytes(np, tw);
+#define GNOT_X6W(NP_, TW_)                                                                                     \
+  if (np == NP_ && tw == TW_) {                                                                                \
     static bool attr = false;                                                                                  \
     if (!attr) {                                                                                               \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(pgemm_x6w_kernel<NP_>),                          \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(pgemm_x6w_kernel<NP_, TW_>),                     \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                         \
       attr = true;                                                                                             \
     }                                                                                                          \
-    hipLaunchKernelGGL((pgemm_x6w_kernel<NP_>), dim3(total_wgs), dim3(kWThreads), lds, s, jobs_dev,            \
+    hipLaunchKernelGGL((pgemm_x6w_kernel<NP_, TW_>), dim3(total_wgs), dim3(w_threads(TW_)), lds, s, jobs_dev,  \
                        wg_prefix_dev, njobs, slab);                                                            \
   }
-    GNOT_X6W(3) GNOT_X6W(1)
+    GNOT_X6W(3, 256) GNOT_X6W(1, 256) GNOT_X6W(3, 128) GNOT_X6W(1, 128)
 #undef GNOT_X6W
   } else if (x6) {
     if (np == 1) hipLaunchKernelGGL(pgemm_x6_kernel<1>, dim3(total_wgs), dim3(256), 0, s, jobs_dev, wg_prefix_dev, njobs, slab);
