@@ -258,8 +258,17 @@ GNOT_DEV void c2f_layer(C2Pipe& pp, const u32x4* W, const u32x4 (&in)[KBI][NP], 
   constexpr int TU = c2_tile_u4(KBI, NP);
   const u32x4* bias = pp.lds + C2Lds<256, NP>::kBias + bsel * 64;
   f32x4 prev;
+  // B16 saves in pair mode: the two 8-byte halves of a 16-byte pair-interleaved chunk (tiles 2t, 2t+1) go out
+  // as ONE store once the odd tile's epilogue is done (the even tile's half waits in `held`): half the store
+  // instructions of 8-byte tile stores (MI355X_MICROARCH.md: narrow stores are issue-bound)
+  constexpr bool COMB = B16 && SAVE && c2f_pair<NP>();
+  u32x2 held;
   auto save_tile = [&](int o, const f32x4& acc) {
-    if constexpr (B16) {
+    if constexpr (COMB) {
+      const u32x2 w = u32x2{pk_bf16(acc[0], acc[1]), pk_bf16(acc[2], acc[3])};
+      if ((o & 1) == 0) held = w;
+      else buf_store_b128(u32x4{held[0], held[1], w[0], w[1]}, rs, voff + ((o >> 1) * 4 + g) * 16);
+    } else if constexpr (B16) {
       const float v[4] = {acc[0], acc[1], acc[2], acc[3]};
       store_tile_b16(v, rs, voff, o, g);
     } else {
@@ -302,8 +311,10 @@ GNOT_DEV void c2f_layer(C2Pipe& pp, const u32x4* W, const u32x4 (&in)[KBI][NP], 
 #ifdef GNOT_DIAG_STAMP
     const unsigned long long t0 = pp.stamp_in();
 #endif
+    // stores issued after the DMA being retired (issued at pair o-2): the saves of tiles o-3 and o-2 (COMB: the
+    // one combined store of tiles o-4, o-3)
     if (o == 0) c2_sync_n(pend0);
-    else c2_sync_n(SAVE ? (o >= 4 ? 2 : 1) : 0);
+    else c2_sync_n(SAVE ? (COMB ? (o >= 4 ? 1 : 0) : (o >= 4 ? 2 : 1)) : 0);
 #ifdef GNOT_DIAG_STAMP
     pp.stamp_out(t0);
 #endif
@@ -419,8 +430,9 @@ __global__ void __launch_bounds__(64 * kC2Waves, 2) chain2_fwd_kernel(ChainArgs 
   C2Pipe pp{c2lds, LD::WB, 0, wave, lane};
   constexpr int CH = c2f_pair<NP>() ? 2 : 1;         // output tiles per weight chunk
   // a layer's first wait: the saves the previous layer issued after its last weight DMA (its last
-  // tile's stream + the final epilogue; pair mode: its last pair's two tiles + the final epilogue)
-  constexpr int pend_next = SAVE ? (CH == 2 ? 3 : 2) : 0;
+  // tile's stream + the final epilogue; pair mode: its last pair's two tiles + the final epilogue; B16 pair
+  // mode: the combined stores of tiles 12-13 and 14-15)
+  constexpr int pend_next = SAVE ? (CH == 2 ? (B16 ? 2 : 3) : 2) : 0;
   constexpr int e_begin = 0;
   auto expert = [&](int e) __attribute__((always_inline)) {
   const ChainLayer* L = a.layers + e * nl;
@@ -627,10 +639,19 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP],
   };
   // tile o's dz store is issued at the top of tile o+2, after that tile's DMAs: a counted wait only
   // retires the ops issued before the DMA it waits for, so each store gets two tiles to drain
+  // B16: one 16-byte store per tile PAIR (the pair-interleaved chunk of tiles o-1, o), at odd o
   auto stores = [&](int o) {
-    if constexpr (B16) store_tile_b16(nx[o], rz, voff, o, g);
-    else buf_store_f32x4(make_float4(nx[o][0], nx[o][1], nx[o][2], nx[o][3]), rz, voff + 64 * o);
-    ++pp.issued;
+    if constexpr (B16) {
+      if (o & 1) {
+        buf_store_b128(u32x4{pk_bf16(nx[o - 1][0], nx[o - 1][1]), pk_bf16(nx[o - 1][2], nx[o - 1][3]),
+                             pk_bf16(nx[o][0], nx[o][1]), pk_bf16(nx[o][2], nx[o][3])},
+                       rz, voff + ((o >> 1) * 4 + g) * 16);
+        ++pp.issued;
+      }
+    } else {
+      buf_store_f32x4(make_float4(nx[o][0], nx[o][1], nx[o][2], nx[o][3]), rz, voff + 64 * o);
+      ++pp.issued;
+    }
   };
   // does tile t request saved rows (fp32: tile t + 2; B16: at even t, pair t / 2 + PK)?
   auto hdma = [&](int t) { return B16 ? ((t & 1) == 0 && (t / 2 + PK < DT / 2 || has_next_h))
