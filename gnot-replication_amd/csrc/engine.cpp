@@ -231,6 +231,9 @@ struct gnot_plan {
   // operand pieces of the kernels this plan runs: the bf16 mode covers every width up to 256 (chain.hip /
   // linear.hip / the 128-tile weight gradients at d <= 192 as well); above 256 (chainw.hip) the fp32 path
   int npk() const { return D <= 256 ? np : 3; }
+  // linear.hip's image kind of the attention projections (LinearArgs::img): d <= 192 one-piece (bf16 mode) or
+  // x6 (kLinearX6), else fp32 fragment images (also d > 256)
+  int lin_img() const { return D > 192 ? 0 : npk() == 1 ? 1 : kLinearX6 ? 3 : 0; }
   std::string msave(int l, bool m1) const {
     return moe_recompute ? std::string("mrsave") : "b" + std::to_string(l) + (m1 ? ".m1save" : ".m2save");
   }
@@ -533,8 +536,11 @@ static void plan_images(gnot_plan* p) {
   auto attn_imgs = [&](gnot_plan::AttnImgs& A, int iq, int io, const std::vector<int>& ik,
                        const std::vector<int>& iv, bool selftype) {
     const int D = p->D;
-    const int x6 = c2 ? c2x6 : b1 ? 3 : 0;
-    auto img = [&](int OT, int KT) { return c2 ? new_img_x6(OT, KT, c2np) : b1 ? new_img_x6(OT, KT, 1) : new_img(OT, KT); };
+    const bool lx6 = p->lin_img() == 3;   // fp32 mode at d <= 192 (kLinearX6): output-major x6
+    const int x6 = c2 ? c2x6 : b1 ? 3 : lx6 ? 2 : 0;
+    auto img = [&](int OT, int KT) {
+      return c2 ? new_img_x6(OT, KT, c2np) : b1 ? new_img_x6(OT, KT, 1) : lx6 ? new_img_x6(OT, KT, 3) : new_img(OT, KT);
+    };
     if (selftype) {
       A.qkv = img(3 * DT, DT);
       A.bqkv = new_bias(3 * D);
@@ -1544,7 +1550,7 @@ int run_linear(Ctx& c, const float* X, long ldx, int K, const Img& A, const floa
   LinearArgs a{};
   a.nseg = 1; a.X[0] = X; a.Wp[0] = A.p; a.ldx = ldx; a.nsum = 1; a.sum_stride = 0; a.K = K;
   a.bias = bias; a.Y = Y; a.ldy = ldy; a.NO = NO; a.P = (int)P;
-  a.epi = epi; a.nsoft = nsoft; a.dh = c.p->dh; a.np = c.p->npk();
+  a.epi = epi; a.nsoft = nsoft; a.dh = c.p->dh; a.np = c.p->npk(); a.img = c.p->lin_img();
   a.dreal = (nsoft > 0 && c.p->padded()) ? c.p->Dr : 0;
   a.ncol = ncol;
   GNOT_CK(c.p->D == 256 ? launch_linear2(a, c.s) : launch_linear(a, c.p->D, c.s));
@@ -1562,7 +1568,7 @@ int run_linear_seg(Ctx& c, std::initializer_list<std::pair<const float*, const I
     ++a.nseg;
   }
   a.ldx = ldx; a.nsum = 1; a.K = c.p->D; a.bias = nullptr; a.Y = Y; a.ldy = ldy; a.NO = c.p->D; a.P = (int)P;
-  a.epi = epi; a.nsoft = 0; a.dh = c.p->dh; a.np = c.p->npk();
+  a.epi = epi; a.nsoft = 0; a.dh = c.p->dh; a.np = c.p->npk(); a.img = c.p->lin_img();
   GNOT_CK(c.p->D == 256 ? launch_linear2(a, c.s) : launch_linear(a, c.p->D, c.s));
   return GNOT_OK;
 }

@@ -52,6 +52,9 @@ struct LinearArgs {
   int nsoft;                         // feature-softmax on output columns [0, nsoft)
   int dh;                            // head width for that softmax
   int np = 3;                        // linear2: operand pieces (3 = bf16x6, 1 = bf16 mode)
+  // linear.hip (d <= 192): 0 = fp32 fragment images on the fp32 MFMA; 1 / 3 = output-major bf16-piece images
+  // (the bf16 mode / the fp32 mode's bf16x6, kLinearX6)
+  int img = 0;
   // padded hidden width (the plan runs a real width dr < D in tiles of D, engine.cpp gnot_plan_create):
   // output column c with c % D >= dreal is written as 0 (the softmax of a head's features must not leak
   // into the pad columns, which the next kernels read as exact zeros); 0 = no pad columns
@@ -138,6 +141,14 @@ struct ChainArgs {
 constexpr bool kChainBwdX6 = false;
 #else
 constexpr bool kChainBwdX6 = true;
+#endif
+// d <= 192 projections in the fp32 mode: bf16x6 on output-major 3-piece images (pack x6 = 2), as linear2.hip
+// at d = 256; -DGNOT_LINEAR_FP32 builds the round-1..4 form (exact fp32 MFMA on fp32 fragment images).
+// configs[1] (d = 128), one box, interleaved x2: 3.37 / 3.35 ms per step against 3.44 / 3.44 (profiles/r05o*)
+#ifdef GNOT_LINEAR_FP32
+constexpr bool kLinearX6 = false;
+#else
+constexpr bool kLinearX6 = true;
 #endif
 // walk or per-expert grid for a MoE call of P points (env GNOT_MOE_WALK = 0 / 1 forces, read per call)
 bool chain2_walk_choice(long P, int E);

@@ -17,56 +17,73 @@
 
 namespace gnot {
 
-// bf16 arithmetic mode (NP = 1): the images are OUTPUT-MAJOR one-piece bf16 (pack x6 = 3, as linear2.hip's):
-// block (o, kb) = 16 outputs x 32 contraction slots at Wg[(o * KB + kb) * 64 + lane], so a workgroup's OC
-// output tiles are one contiguous run of OC * KB blocks.  Chunks of OCH tiles (OCH * KB <= 16 blocks = one
-// 16 KiB buffer) stream through the same two LDS buffers as the fp32 pipe; the input is rounded to bf16
-// once per segment (bp, one 16x16x32 B operand per k-block), one v_mfma_f32_16x16x32_bf16 per block
-constexpr int b1_och(int KB, int OC) {
+// NP-piece forms (round 5): the images are OUTPUT-MAJOR bf16 pieces (pack x6 = 3 for one RNE piece, the
+// bf16 arithmetic mode; x6 = 2 for the exact three-piece split of the fp32 mode, kLinearX6, as linear2.hip's): block (o, kb) = 16 outputs x 32 contraction slots, piece q at Wg[((o * KB + kb) * NP + q) *
+// 64 + lane], so a workgroup's OC output tiles are one contiguous run of OC * KB blocks.  Chunks of OCH tiles
+// (OCH * KB * NP KiB <= the buffer) stream through two LDS buffers; the input is split once per segment (bp,
+// NP 16x16x32 B operands per k-block); per block one v_mfma_f32_16x16x32_bf16 (NP = 1) or the six order <= 2
+// piece products (NP = 3, smallest first)
+template <int NP>
+constexpr int bx_buf_kb() { return NP == 1 ? kChunkKB : 24; }
+template <int NP>
+constexpr int bx_och(int KB, int OC) {
   int c = OC;
-  while (c > 1 && (c * KB > kChunkKB || OC % c != 0)) --c;
+  while (c > 1 && (c * KB * NP > bx_buf_kb<NP>() || OC % c != 0)) --c;
   return c;
 }
-constexpr int b1_chunk_f4(int KB, int OC) { return b1_och(KB, OC) * KB * WAVE; }
-template <int KB, int OC, typename Hook = NoHook>
-GNOT_DEV void mm_tiles_pipe_b1(const float4* __restrict__ Wg, const float4* __restrict__ next_W, int next_f4,
-                               float4* lds, int& cnt, const u32x4 (&bp)[KB], f32x4 (&acc)[OC], int nwaves, int wave,
-                               int lane, Hook hook = Hook()) {
-  constexpr int OCH = b1_och(KB, OC);
+template <int NP>
+constexpr int bx_chunk_f4(int KB, int OC) { return bx_och<NP>(KB, OC) * KB * NP * WAVE; }
+template <int KB, int OC, int NP, typename Hook = NoHook>
+GNOT_DEV void mm_tiles_pipe_bx(const float4* __restrict__ Wg, const float4* __restrict__ next_W, int next_f4,
+                               float4* lds, int& cnt, const u32x4 (&bp)[KB][NP], f32x4 (&acc)[OC], int nwaves,
+                               int wave, int lane, Hook hook = Hook()) {
+  constexpr int OCH = bx_och<NP>(KB, OC);
   constexpr int NC = OC / OCH;
-  constexpr int CH4 = OCH * KB * WAVE;
+  constexpr int CH4 = OCH * KB * NP * WAVE;
+  constexpr int BUF4 = bx_buf_kb<NP>() * WAVE;
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     lds_dma_wait();                                    // this chunk's DMA (issued one chunk ago) has landed
     __syncthreads();
-    float4* nb = lds + ((cnt + 1) & 1) * kChunkF4;
+    float4* nb = lds + ((cnt + 1) & 1) * BUF4;
     if (c + 1 < NC) stage_image(nb, Wg + (c + 1) * CH4, CH4, nwaves, wave, lane);
     else if (next_W) stage_image(nb, next_W, next_f4, nwaves, wave, lane);
     if (c == 0) hook();
-    const u32x4* cb = reinterpret_cast<const u32x4*>(lds + (cnt & 1) * kChunkF4);
+    const u32x4* cb = reinterpret_cast<const u32x4*>(lds + (cnt & 1) * BUF4);
 #pragma unroll
     for (int o = 0; o < OCH; ++o) {
       f32x4 r = acc[c * OCH + o];
 #pragma unroll
-      for (int kb = 0; kb < KB; ++kb) r = mfma_bf16(cb[(o * KB + kb) * WAVE + lane], bp[kb], r);
+      for (int kb = 0; kb < KB; ++kb) {
+        const u32x4* blk = cb + (o * KB + kb) * NP * WAVE + lane;
+        if constexpr (NP == 3) {
+          r = mfma_bf16(blk[2 * WAVE], bp[kb][0], r);
+          r = mfma_bf16(blk[WAVE], bp[kb][1], r);
+          r = mfma_bf16(blk[0], bp[kb][2], r);
+          r = mfma_bf16(blk[WAVE], bp[kb][0], r);
+          r = mfma_bf16(blk[0], bp[kb][1], r);
+        }
+        r = mfma_bf16(blk[0], bp[kb][0], r);
+      }
       acc[c * OCH + o] = r;
     }
     ++cnt;
   }
 }
 
-template <int D, int OC, int NP = 3>   // OC: output tiles per workgroup (grid.y splits NO)
+// NP: 0 = fp32 fragment images on the exact fp32 MFMA; 1 / 3 = the output-major bf16-piece forms above
+template <int D, int OC, int NP = 0>   // OC: output tiles per workgroup (grid.y splits NO)
 GNOT_DEV void linear_body(const LinearArgs& a, float4* wlds) {
   constexpr int KT = D / 16, KB = (KT + 1) / 2;
-  constexpr bool B1 = NP == 1;
+  constexpr bool B1 = NP > 0;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const long p = ((long)blockIdx.x * 4 + wave) * 16 + (lane & 15);
   const bool valid = p < a.P;
   const int c = blockIdx.y;                       // output chunk of this workgroup
   // chunk offset inside every segment's image (fp32 tiles of KT x 1 KiB, or KB one-piece blocks per tile)
-  const long wchunk = (long)c * OC * (B1 ? KB : KT) * WAVE;
-  const int cf4 = B1 ? b1_chunk_f4(KB, OC) : chunk_f4(KT, OC);
+  const long wchunk = (long)c * OC * (B1 ? KB * NP : KT) * WAVE;
+  const int cf4 = B1 ? bx_chunk_f4<B1 ? NP : 1>(KB, OC) : chunk_f4(KT, OC);
   int cnt = 0;
   stage_image(wlds, a.Wp[0] + wchunk, cf4, 4, wave, lane);
 
@@ -92,15 +109,11 @@ GNOT_DEV void linear_body(const LinearArgs& a, float4* wlds) {
       if (more) load_rows<KT>(nx, a.X[sg + 1], a.ldx, p, valid, a.K, lane);
     };
     if constexpr (B1) {
-      u32x4 bp[KB];
+      u32x4 bp[KB][NP];
 #pragma unroll
-      for (int kb = 0; kb < KB; ++kb) {
-        u32x4 t[1];
-        split_block_x6<KT, 1>(in, kb, t);
-        bp[kb] = t[0];
-      }
-      mm_tiles_pipe_b1<KB, OC>(a.Wp[sg] + wchunk, more ? a.Wp[sg + 1] + wchunk : nullptr, cf4, wlds, cnt, bp, acc, 4,
-                               wave, lane, pre);
+      for (int kb = 0; kb < KB; ++kb) split_block_x6<KT, NP>(in, kb, bp[kb]);
+      mm_tiles_pipe_bx<KB, OC, NP>(a.Wp[sg] + wchunk, more ? a.Wp[sg + 1] + wchunk : nullptr, cf4, wlds, cnt, bp, acc,
+                                   4, wave, lane, pre);
     } else {
       mm_tiles_pipe<KT, OC>(a.Wp[sg] + wchunk, more ? a.Wp[sg + 1] + wchunk : nullptr, cf4, wlds, cnt, in, acc, 4,
                             wave, lane, pre);
@@ -137,9 +150,9 @@ GNOT_DEV void linear_body(const LinearArgs& a, float4* wlds) {
   store_rows<OC>(h, Y, a.ldy, p, valid, ncols, lane);
 }
 
-template <int D, int OC, int NP = 3>
+template <int D, int OC, int NP = 0>
 __global__ void __launch_bounds__(256) linear_kernel(LinearArgs a) {
-  __shared__ __attribute__((aligned(16))) float4 wlds[2 * pipe_buf_f4<D / 16>()];
+  __shared__ __attribute__((aligned(16))) float4 wlds[2 * (NP == 3 ? bx_buf_kb<3>() * WAVE : pipe_buf_f4<D / 16>())];
   linear_body<D, OC, NP>(a, wlds);
 }
 
@@ -208,13 +221,15 @@ hipError_t launch_linear(const LinearArgs& a, int D, hipStream_t s) {
   const dim3 grid((a.P + 63) / 64, a.NO / (16 * oc)), block(256);
 #define GNOT_LIN(DD, OO) \
   if (D == DD && oc == OO) { hipLaunchKernelGGL((linear_kernel<DD, OO>), grid, block, 0, s, a); return hipGetLastError(); }
-  // bf16 mode (a.np == 1) at d <= 192: one-piece output-major images (the d = 256 projections are linear2.hip's)
+  // d <= 192 on output-major bf16-piece images (LinearArgs::img): the bf16 mode (1) and the fp32 mode's bf16x6
+  // (3, kLinearX6); the d = 256 projections are linear2.hip's
 #define GNOT_LIN_B1(DD, OO)                                                                              \
   if (D == DD && oc == OO) {                                                                              \
-    hipLaunchKernelGGL((linear_kernel<DD, OO, 1>), grid, block, 0, s, a);                                 \
+    if (a.img == 1) hipLaunchKernelGGL((linear_kernel<DD, OO, 1>), grid, block, 0, s, a);                 \
+    else hipLaunchKernelGGL((linear_kernel<DD, OO, 3>), grid, block, 0, s, a);                            \
     return hipGetLastError();                                                                             \
   }
-  if (a.np == 1) {
+  if (a.img == 1 || a.img == 3) {
     if (D > 192) return hipErrorInvalidValue;
     GNOT_LIN_B1_CASES
     return hipErrorInvalidValue;
