@@ -118,19 +118,22 @@ GNOT_DEV void round_rows_bf16(float (&a)[KT][4]) {
     for (int r = 0; r < 4; ++r) a[T][r] = bf16_lo(pk_bf16(a[T][r], 0.f));
 }
 
-// The fused soft-MoE combine (model.py:128-131 / 134-137), OPT-IN (GNOT_MOE_FUSED=1, engine.cpp moe_fused):
-// called by every workgroup of the expert grid after its write-through (sc1) stage stores.  Every wave waits
-// for its own stores (vmcnt(0)), a barrier, then ONE lane runs an agent-scope release and adds to the block's
-// counter (agent scope) for the whole workgroup; the workgroup whose add returns E - 1 is the last: that lane
-// resets the counter for the next launch, runs ONE agent-scope acquire and waits for it before the barrier
-// its siblings join, then the workgroup sums the block's E stage rows with sc1 loads, in expert order, onto
-// `base` (or 0): bitwise the separate combine pass.  This is MI355X_MICROARCH.md's general form, valid
-// whatever else shares the CUs (round 4 relied on sc1 stores + loads alone, valid only with one workgroup
-// per CU).  The wrong gradients that put it under suspicion (r04sf, r05c, r05d: the 2-rank sharded 70k test)
+// The fused soft-MoE combine (model.py:128-131 / 134-137): called by every workgroup of the expert grid after
+// its write-through (sc1) stage stores.  Every wave waits for its own stores (vmcnt(0)), a barrier, then ONE
+// lane adds to the block's counter (agent scope) for the whole workgroup; the workgroup whose add returns
+// E - 1 is the last: that lane resets the counter for the next launch, runs ONE agent-scope acquire and waits
+// for it before the barrier its siblings join, then the workgroup sums the block's E stage rows with sc1
+// loads, in expert order, onto `base` (or 0): bitwise the separate combine pass.
+// Form (MI355X_MICROARCH.md "Valid forms"): sc1 stores drained by every storing wave before the workgroup's
+// signal are the producer side without an agent release ((2) and (3)); the consumer keeps the acquire, so
+// the form does not depend on one workgroup per CU (condition (4), which only licenses dropping the acquire,
+// as round 4 did).  It holds beside co-resident work: the side-stream weight gradients, RCCL kernels, another
+// process.  The wrong gradients that put it under suspicion (r04sf, r05c, r05d: the 2-rank sharded 70k test)
 // came from the TEST's host-staged collectives, which read device buffers before the kernels writing them
-// had finished (gnot_amd/parallel.py PointShardComm, fixed): they reproduced with this combine switched off.
-// The release costs ~1 ms per chain backward and ~2.3 ms per bf16 chain forward (it writes back the XCD L2's
-// dirty lines once per workgroup), so the default is the combine pass.
+// had finished (gnot_amd/parallel.py PointShardComm, fixed); they reproduced with this combine switched off.
+// An agent release before the counter add (GNOT_MOE_FUSED_RELEASE builds) is not needed by the form and
+// costs ~1 ms per chain backward and ~2.3 ms per bf16 chain forward (it writes back the XCD L2's dirty lines
+// once per workgroup, profiles/r05hf1*).
 template <bool B16>
 GNOT_DEV void moe_combine_last(const float* stage, long stage_stride, int E, const float* base, float* out,
                                int* counters, int blk, long row0, int nrows) {
@@ -138,7 +141,9 @@ GNOT_DEV void moe_combine_last(const float* stage, long stage_stride, int E, con
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
+#ifdef GNOT_MOE_FUSED_RELEASE
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
     const int old = __hip_atomic_fetch_add(counters + blk, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last = old == E - 1;
     if (old == E - 1) {

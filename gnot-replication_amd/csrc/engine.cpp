@@ -217,8 +217,9 @@ struct gnot_plan {
   // soft-MoE calls in the walk form (chain2.hip: one workgroup sums all experts in place, no [P, E, d]
   // stage): decided per batch in gnot_plan_set_batch (chain2_walk_choice)
   bool moe_walk = false;
-  // GNOT_MOE_FUSED=1 (read per batch): the opt-in fused soft-MoE combine (moe_fused)
-  bool moe_fused_env = false;
+  // fused soft-MoE combine policy (moe_fused): 0 never (default), 1 every backward + the bf16-mode forward,
+  // 2 also the bf16x6 forward; GNOT_MOE_FUSED=0/1/2 overrides (read per batch)
+  int moe_fused_mode = 0;
   // input gradients (gnot_plan_set_input_grads): the x / gating / input-function encoders' first Linears
   // also run their backward-data into dxin / dxg / dfnin<i>
   bool input_grads = false;
@@ -1217,7 +1218,7 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
   p->moe_walk = p->D == 256 && p->L > 0 && chain2_walk_choice(P, E);
   {
     const char* f = std::getenv("GNOT_MOE_FUSED");
-    p->moe_fused_env = f && f[0] == '1';
+    p->moe_fused_mode = (f && f[0] >= '0' && f[0] <= '2') ? f[0] - '0' : 0;
   }
   if (!p->moe_walk) C.add("stage", E * P * D, D);
   if (D > 256) {                             // chainw.hip scratch: query-branch chains / input-function branch
@@ -1863,17 +1864,16 @@ int attn_backward(Ctx& c, int l, bool cross) {
 // (262,144 points, E = 8; profiles/r04_chain_grid.txt): bf16x6 forward 6.76 ms + 0.47 pass against 7.51
 // fused, backward 8.27 + 0.47 against 8.73; bf16 storage forward 4.01 + 0.47 against 4.08 fused
 static bool moe_walk(gnot_plan* p) { return p->moe_walk; }
-// The expert grid's fused combine (an inter-workgroup hand-off of a block's stage rows to its last
-// workgroup, chain2.hip moe_combine_last) is OPT-IN since round 5 (GNOT_MOE_FUSED=1, read per batch, plans
-// with serial weight gradients).  In the guide's general form (agent release before the counter add, agent
-// acquire in the last workgroup) it is valid beside any co-resident work, but the release writes back the
-// XCD L2's dirty lines of every workgroup: measured on one box, interleaved x2 (profiles/r05h_*), fp32 chain
-// backward 10.24 / 10.27 ms fused vs 9.18 / 9.19 + the pass, step 238.7 / 239.3 vs 234.2 / 234.9 ms; bf16
-// mode 122.6 / 122.7 vs 97.4 / 97.0 ms.  So every soft-MoE call sums its stage with the moe_combine pass --
-// a kernel boundary, no hand-off (the bf16 mode over bf16 stage rows, moe_combine_b16).  Every form gives the
-// same bits (tests/test_gpu_moe_walk.py, test_gpu_recompute.py)
+// The expert grid's fused combine (the last workgroup of a 128-point block sums its E stage rows, chain2.hip
+// moe_combine_last: sc1 stores, counter, agent acquire -- valid beside any co-resident work) or the
+// moe_combine pass (bf16 mode: moe_combine_b16 over bf16 stage rows).  Every form gives the same bits
+// (tests/test_gpu_moe_walk.py, test_gpu_recompute.py).  Default: the pass.  One box, interleaved x2
+// (profiles/r05rf*): configs[2] fp32 229.9 / 230.4 ms (pass) vs 230.7 / 230.0 (fused backward) vs 232.9 /
+// 232.3 (fused everywhere); bf16 mode 92.6 / 93.3 vs 95.9 / 95.9 (the bf16 pass reads bf16 stage rows);
+// configs[0] 9.24 vs 9.30 ms, bf16 5.93 vs 6.13
 static bool moe_fused(gnot_plan* p, bool bwd) {
-  return p->moe_fused_env && p->D == 256 && !p->moe_walk && p->serial_wgrad() && (bwd || p->b16s());
+  if (p->D != 256 || p->moe_walk || p->moe_fused_mode == 0) return false;
+  return p->moe_fused_mode == 2 || bwd || p->b16s();
 }
 // the bf16 mode's expert grid with the combine pass: bf16 stage rows and moe_combine_b16
 static bool moe_stage_b16(gnot_plan* p, bool bwd) { return p->b16s() && !p->moe_walk && !moe_fused(p, bwd); }
