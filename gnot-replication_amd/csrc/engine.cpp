@@ -1059,9 +1059,6 @@ extern "C" int gnot_plan_set_shard(gnot_plan* p, int rank, int world, int B, con
     p->world = 1; p->rank = 0; p->nglob.clear(); p->comm = gnot_comm{};
     return GNOT_OK;
   }
-  if (p->padded())
-    return fail(GNOT_E_INVALID, "point sharding needs a hidden width the kernels run unpadded (a multiple of 16 up "
-                                "to 192, or 256)");
   if (rank < 0 || rank >= world || B <= 0 || !n_global || !comm->allreduce_sum || !comm->alltoallv)
     return fail(GNOT_E_INVALID, "bad shard arguments");
   p->world = world;

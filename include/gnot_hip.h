@@ -180,7 +180,7 @@ int gnot_plan_set_grad_comm(gnot_plan* plan, const gnot_comm* comm);
 /* Declare the rank's shard of the next batch: n_global[b] = points of sample b over all ranks.
  * Call before gnot_plan_set_batch, whose x_off then gives the LOCAL slices (validated against
  * gnot_shard_range).  world == 1 (or comm == NULL) switches sharding off.  `comm` is copied.
- * A padded hidden width (see gnot_config) is refused (GNOT_E_INVALID). */
+ * Padded hidden widths (see gnot_config) shard too: the exchanges move the real width's rows. */
 int gnot_plan_set_shard(gnot_plan* plan, int rank, int world, int B, const int64_t* n_global, const gnot_comm* comm);
 
 /* Host-only helpers (no GPU): the canonical point range of a rank, and the rank's side of the

@@ -111,6 +111,25 @@ def _rank(rank, world, port, cfg, Ns, Ms, q, backend="gloo", fx=None, env=None):
              Ns=[64, 5], Ms=[[20, 9], [7, 12]])),
 ])
 def test_point_sharded_gnot_matches_oracle(world, case):
+    _run_sharded_case(world, case)
+
+
+@pytest.mark.parametrize("world,case", [
+    # padded hidden widths (the kernels run D > d with exact-zero pad columns; the scramble rows, the states
+    # and the exchange tables use the real width d = H * dh): d = 100 (5 heads of 20, kernels at 112) and
+    # d = 208 (13 heads of 16, the d = 256 kernels)
+    (2, dict(cfg=dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=2, n_attn_layers=2, d=100,
+                      n_mlp_num_layers=2, n_expert=3, n_head=5, n_input_functions=1),
+             Ns=[150, 97], Ms=[[40, 31]])),
+    (3, dict(cfg=dict(input_dim=3, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=1, d=208,
+                      n_mlp_num_layers=2, n_expert=2, n_head=13, n_input_functions=0),
+             Ns=[131, 40], Ms=[])),
+])
+def test_point_sharded_padded_widths(world, case):
+    _run_sharded_case(world, case)
+
+
+def _run_sharded_case(world, case):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
