@@ -19,6 +19,8 @@
 //             layer: CH_STORE / CH_SOFTMAX (gating) / CH_MOE (score-scaled expert output)
 //   backward: dz_{nl-1} = dy (x score for CH_MOE), g_l = W_l^T dz_l, dz_{l-1} = g_l * gelu'(h_{l-1});
 //             writes every dz_l (weight gradients, wgrad.hip) and optionally dX = W_0^T dz_0.
+#include <cstdlib>
+
 #include "gnot_kernels.h"
 #include "x6_core.h"
 
@@ -39,6 +41,18 @@ template <int NP, bool B16>
 constexpr int c2b_ch() { return (B16 && NP == 1) ? 2 : 1; }
 // bf16-storage backward: saved-row tile pairs requested this many pairs ahead (r03r: 6 vs 1 neutral)
 constexpr int kC2bPairsAhead = 6;
+
+// diagnostic builds only (make microbench EXTRA=-DGNOT_DIAG_STAMP): runtime switches that make the chains
+// compute WRONG results, to price one part of their work -- bit 1: no GELU (identity), bit 2: every save /
+// dZ / stage store dropped by a zero-size buffer resource (still issued and counted), bit 4: no weight-chunk
+// DMA after the prologue
+#ifdef GNOT_DIAG_STAMP
+__constant__ int c2_diag;
+hipError_t set_chain2_diag(int v) { return hipMemcpyToSymbol(HIP_SYMBOL(c2_diag), &v, sizeof(int)); }
+#define C2D(bit) (c2_diag & (bit))
+#else
+#define C2D(bit) 0
+#endif
 
 
 // LDS of one workgroup (u32x4 units): two weight-chunk buffers, two 1 KiB bias buffers (layer parity,
@@ -79,14 +93,31 @@ GNOT_DEV void c2_grid_pos(int E, int mode, int& blk, int& e) {
     e = (int)blockIdx.y;
     return;
   }
+  // mode K >= 1: K experts per XCD.  The E experts form E / K groups of K; XCD x serves group x % (E / K)
+  // (R = 8 / (E / K) XCDs per group, replica x / (E / K)), running the group's K experts of a block at the
+  // same time.  K = E is the "grouped" deal above
+  const int K = mode, XG = E / K, R = 8 / XG;
   const int w = (int)blockIdx.x, x = w & 7, s = w >> 3;
-  e = s % E;
-  blk = (s / E) * 8 + x;
+  e = (x % XG) * K + s % K;
+  blk = (s / K) * R + x / XG;
 }
-// the grid mode of an expert grid of E chains
-static int c2_grid_mode(int E) { return E <= 1 ? 0 : 1; }
-// 1-D grid of mode 1 (the ids past the last block exit at once)
-inline unsigned c2_grid_size(int nblocks, int E) { return (unsigned)((nblocks + 7) / 8 * 8) * (unsigned)E; }
+// the grid mode of an expert grid of E chains: K experts per XCD (GNOT_C2_XCD_EXPERTS; K must divide E
+// and E / K divide 8, else K = E)
+static int c2_grid_mode(int E) {
+  if (E <= 1) return 0;
+  static const int k_env = [] {
+    const char* v = std::getenv("GNOT_C2_XCD_EXPERTS");
+    return v ? std::atoi(v) : 0;
+  }();
+  const int K = k_env;
+  if (K >= 1 && K <= E && E % K == 0 && 8 % (E / K) == 0) return K;
+  return E;
+}
+// 1-D grid of mode K (the ids past the last block exit at once)
+inline unsigned c2_grid_size(int nblocks, int E, int K) {
+  const int R = 8 / (E / K);
+  return 8u * (unsigned)K * (unsigned)((nblocks + R - 1) / R);
+}
 
 // OT point-form tiles of this lane's row (rows of 256 fp32, voff = row-in-block * 1 KiB + 16 B * g) stored
 // write-through (sc1: the bytes reach the device-coherent level, so another XCD's sc1 loads see them)
@@ -289,7 +320,8 @@ GNOT_DEV void c2f_layer(C2Pipe& pp, const u32x4* W, const u32x4 (&in)[KBI][NP], 
     if (SAVE && !SGRAD) save_tile(o, acc);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      if constexpr (SGRAD) out[o][r] = gelu_and_grad(acc[r], gd[r]);
+      if (C2D(1)) { out[o][r] = acc[r]; gd[r] = acc[r]; }
+      else if constexpr (SGRAD) out[o][r] = gelu_and_grad(acc[r], gd[r]);
       else out[o][r] = GELU ? gelu(acc[r]) : acc[r];
     }
     pin4(out[o]);
@@ -299,7 +331,11 @@ GNOT_DEV void c2f_layer(C2Pipe& pp, const u32x4* W, const u32x4 (&in)[KBI][NP], 
   // part 3)
   auto epi_part = [&](int o, const f32x4& acc, int r) {
     if (SAVE && !SGRAD && r == 0) save_tile(o, acc);
-    if constexpr (SGRAD) {
+    if (C2D(1)) {
+      out[o][r] = acc[r]; gd[r] = acc[r];
+      asm volatile("" : "+v"(out[o][r]), "+v"(gd[r]));
+      if (SAVE && SGRAD && r == 3) save_tile(o, f32x4{gd[0], gd[1], gd[2], gd[3]});
+    } else if constexpr (SGRAD) {
       out[o][r] = gelu_and_grad(acc[r], gd[r]);
       asm volatile("" : "+v"(out[o][r]), "+v"(gd[r]));
       if (SAVE && r == 3) save_tile(o, f32x4{gd[0], gd[1], gd[2], gd[3]});
@@ -327,6 +363,7 @@ GNOT_DEV void c2f_layer(C2Pipe& pp, const u32x4* W, const u32x4 (&in)[KBI][NP], 
     u32x4* nb = pp.nxt();
     ++pp.cnt;
     auto issue = [&]() __attribute__((always_inline)) {
+      if (C2D(4)) return;
       if (o + 3 < OT) {
         dma_image_n<2 * TU, kC2Waves>(nb, W + (size_t)(o + 2) * TU, pp.wave, pp.lane);
       } else if (o + 2 < OT) {
@@ -375,6 +412,7 @@ GNOT_DEV void c2f_layer(C2Pipe& pp, const u32x4* W, const u32x4 (&in)[KBI][NP], 
     u32x4* nb = pp.nxt();
     ++pp.cnt;
     auto issue = [&]() __attribute__((always_inline)) {
+      if (C2D(4)) return;
       if (o + 1 < OT) {
         dma_image_n<TU, kC2Waves>(nb, W + (size_t)(o + 1) * TU, pp.wave, pp.lane);
       } else if (nextW) {
@@ -451,12 +489,13 @@ __global__ void __launch_bounds__(64 * kC2Waves, 2) chain2_fwd_kernel(ChainArgs 
   dma_image(c2lds, W0, CH * c2_tile_u4(KB0, NP), kC2Waves, wave, lane);
   auto wp = [&](int l) { return reinterpret_cast<const u32x4*>(L[l].Wp); };
   auto rs = [&](int l) {
-    return make_rsrc(SAVE ? save + l * a.save_layer_stride + rbase : nullptr, SAVE ? (B16 ? lay_b16 : lay_bytes) : 0u);
+    return make_rsrc(SAVE ? save + l * a.save_layer_stride + rbase : nullptr,
+                     SAVE && !C2D(2) ? (B16 ? lay_b16 : lay_bytes) : 0u);
   };
   const int svoff = B16 ? rowb : voff;
   // B16: a Linear's bf16 input words (k-blocks 0 .. nkb-1) into save slot `slot`; returns the stores issued
   auto store_in = [&](const float* slot, const u32x4 (&w)[KB][NP], int nkb) __attribute__((always_inline)) {
-    const rsrc_t r = make_rsrc(slot + rbase, lay_b16);
+    const rsrc_t r = make_rsrc(slot + rbase, C2D(2) ? 0u : lay_b16);
 #pragma unroll
     for (int t = 0; t < KB; ++t)
       if (t < nkb) buf_store_b128(w[t][0], r, rowb + (t * 4 + g) * 16);
@@ -570,7 +609,7 @@ __global__ void __launch_bounds__(64 * kC2Waves, 2) chain2_fwd_kernel(ChainArgs 
     }
     if constexpr (B16) {
       if (a.stage_b16 && a.Y != nullptr) {    // bf16 stage rows for the moe_combine_b16 pass
-        store_rows_b16<OTL>(y, make_rsrc(a.Y + e * a.y_chain_stride + rbase, lay_b16), rowb, lane);
+        store_rows_b16<OTL>(y, make_rsrc(a.Y + e * a.y_chain_stride + rbase, C2D(2) ? 0u : lay_b16), rowb, lane);
         return;
       }
     }
@@ -634,7 +673,7 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP],
       h = hc[r];
     }
     // B16: the forward stored gelu'(h_{l-1}) itself (c2f_layer SGRAD)
-    nx[o][r] = acc[r] * (B16 ? h : gelu_grad(h));
+    nx[o][r] = acc[r] * ((B16 || C2D(1)) ? h : gelu_grad(h));
     asm volatile("" : "+v"(nx[o][r]));
   };
   // the saved tile of tile o's epilogue, read from its slot
@@ -699,7 +738,8 @@ GNOT_DEV void c2b_layer(C2Pipe& pp, const u32x4* Wt, const u32x4 (&in)[KBI][NP],
       }
       if (first) {
         const int t = c + LEAD;            // chunk to request
-        if (t < NC) {
+        if (C2D(4)) {
+        } else if (t < NC) {
           dma_image(nb, Wt + (size_t)t * CH * TU, CH * TU, kC2Waves, pp.wave, pp.lane);
           pp.issued += dma_image_count(CH * TU, kC2Waves, pp.wave);
         } else if (nextW && (t - NC) * CH < next_tiles) {
@@ -773,7 +813,7 @@ __global__ void __launch_bounds__(64 * kC2Waves, 2) chain2_bwd_kernel(ChainArgs 
   auto wt = [&](int l) { return reinterpret_cast<const u32x4*>(L[l].WpT); };
   const unsigned lb = B16 ? lay_b16 : lay_bytes;
   auto rh = [&](int l) { return make_rsrc(save + l * a.save_layer_stride + rbase, lb); };   // h_l
-  auto rz = [&](int l) { return make_rsrc(dz + l * a.dz_layer_stride + rbase, lb); };      // dz_l
+  auto rz = [&](int l) { return make_rsrc(dz + l * a.dz_layer_stride + rbase, C2D(2) ? 0u : lb); };      // dz_l
   // prologue DMA: the last Linear's first c2b_lead<NP>() weight chunks (ring buffers 0 ..) and the first
   // two h_{nl-2} tiles (B16: pairs 0 .. kC2bPairsAhead - 1)
   // (h first: a chunk's counted wait retires only the ops older than its DMA)
@@ -899,7 +939,7 @@ __global__ void __launch_bounds__(64 * kC2Waves, 2) chain2_bwd_kernel(ChainArgs 
       if constexpr (B16) store_rows_b16_sc1<KT0>(dx, make_rsrc(a.dX + e * a.dx_chain_stride + rbase, lay_b16), rowb, lane);
       else store_rows_sc1<KT0>(dx, make_rsrc(a.dX + e * a.dx_chain_stride + row0 * D, lay_bytes), voff);
     } else if (B16 && KT0 == 16 && a.stage_b16) {    // bf16 stage rows for the moe_combine_b16 pass
-      store_rows_b16<KT0>(dx, make_rsrc(a.dX + e * a.dx_chain_stride + rbase, lay_b16), rowb, lane);
+      store_rows_b16<KT0>(dx, make_rsrc(a.dX + e * a.dx_chain_stride + rbase, C2D(2) ? 0u : lay_b16), rowb, lane);
     } else {
       if constexpr (B16) round_rows_bf16<KT0>(dx);   // the fused combine's bf16 stage value (see the forward)
       store_rows<KT0>(dx, a.dX + e * a.dx_chain_stride, a.lddx, p, valid, a.in_dim, lane);
@@ -926,7 +966,7 @@ static hipError_t launch_chain2_d(const ChainArgs& a, bool bwd, hipStream_t s) {
   constexpr int DT = D / 16;
   const int nblocks = (a.P + 16 * kC2Waves - 1) / (16 * kC2Waves);
   const int mode = a.walk ? 0 : c2_grid_mode(a.nchains);
-  const dim3 grid = mode ? dim3(c2_grid_size(nblocks, a.nchains)) : dim3(nblocks, a.walk ? 1 : a.nchains);
+  const dim3 grid = mode ? dim3(c2_grid_size(nblocks, a.nchains, mode)) : dim3(nblocks, a.walk ? 1 : a.nchains);
   ChainArgs b = a;
   b.grid_mode = mode;
   const dim3 block(64 * kC2Waves);

@@ -12,6 +12,11 @@
 #include "gnot_kernels.h"
 
 using namespace gnot;
+#ifdef GNOT_DIAG_STAMP
+namespace gnot {
+hipError_t set_chain2_diag(int v);
+}
+#endif
 
 #define CK(x)                                                                                   \
   do {                                                                                          \
@@ -161,6 +166,30 @@ int main(int argc, char** argv) {
     STAMP("chain_bwd b16s+combine", bf, true);
     CK(hipFree(qout));
     CK(hipFree(cnt));
+    // the bf16 mode's default soft-MoE form: bf16 stage rows for the moe_combine_b16 pass
+    ChainArgs a3 = a2, b3 = b2;
+    a3.stage_b16 = 1; a3.y_chain_stride = (long)P * D / 2;
+    b3.stage_b16 = 1; b3.dx_chain_stride = (long)P * D / 2;
+#ifdef GNOT_DIAG_STAMP
+    // priced parts (set_chain2_diag bits: 1 no GELU, 2 stores dropped, 4 no weight DMA); wrong results
+    for (int dg : {0, 1, 2, 4, 3, 6, 7}) {
+      CK(set_chain2_diag(dg));
+      t = time_us([&] { CK(launch_chain_fwd(a3, nullptr)); });
+      const double tf = t;
+      t = time_us([&] { CK(launch_chain_bwd(b3, nullptr)); });
+      std::printf("diag %d  b16s stage   fwd %8.2f us  bwd %8.2f us\n", dg, tf, t);
+      t = time_us([&] { CK(launch_chain_fwd(a, nullptr)); });
+      const double tx = t;
+      t = time_us([&] { CK(launch_chain_bwd(bw, nullptr)); });
+      std::printf("diag %d  fp32 (x6)    fwd %8.2f us  bwd %8.2f us\n", dg, tx, t);
+    }
+    CK(set_chain2_diag(0));
+#else
+    t = time_us([&] { CK(launch_chain_fwd(a3, nullptr)); });
+    std::printf("chain_fwd  b16s stage E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
+    t = time_us([&] { CK(launch_chain_bwd(b3, nullptr)); });
+    std::printf("chain_bwd  b16s stage E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
+#endif
   }
 
   if (argc > 4 && std::atoi(argv[4]) == 1) return 0;   // chains only
