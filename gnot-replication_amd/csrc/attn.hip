@@ -162,7 +162,15 @@ __global__ void __launch_bounds__(256) attn_apply_fwd_kernel(AttnApplyArgs a) {
   float r[C];
 #pragma unroll
   for (int c = 0; c < C; ++c) r[c] = fmaf(os[c], inv_nsrc, qs[c]);
-  store_vec<C>(a.res + off_b * (long)a.H * DH + ((long)t.h * Nb + (t.n - off_b)) * DH + c0, r);
+  if (a.dhr == 0) {
+    store_vec<C>(a.res + off_b * (long)a.H * DH + ((long)t.h * Nb + (t.n - off_b)) * DH + c0, r);
+  } else {
+    // padded heads: the scramble keeps the real head width (its rows are the model's); pad features dropped
+    float* dst = a.res + off_b * (long)a.H * a.dhr + ((long)t.h * Nb + (t.n - off_b)) * a.dhr;
+#pragma unroll
+    for (int c = 0; c < C; ++c)
+      if (c0 + c < a.dhr) dst[c0 + c] = r[c];
+  }
 }
 
 // ---------------------------------------------------------------- apply (backward)
@@ -185,7 +193,13 @@ __global__ void __launch_bounds__(256) attn_apply_bwd_kernel(AttnApplyArgs a) {
   float qf[DH], qs[C], dO[C];
   load_vec<DH>(qf, a.q + t.n * a.ldq + t.h * DH);
   load_vec<C>(qs, a.q + t.n * a.ldq + t.h * DH + c0);
-  load_vec<C>(dO, a.dres + off_b * (long)a.H * DH + ((long)t.h * Nb + (t.n - off_b)) * DH + c0);
+  if (a.dhr == 0) {
+    load_vec<C>(dO, a.dres + off_b * (long)a.H * DH + ((long)t.h * Nb + (t.n - off_b)) * DH + c0);
+  } else {
+    const float* src = a.dres + off_b * (long)a.H * a.dhr + ((long)t.h * Nb + (t.n - off_b)) * a.dhr;
+#pragma unroll
+    for (int c = 0; c < C; ++c) dO[c] = c0 + c < a.dhr ? src[c0 + c] : 0.f;
+  }
   float dq[C];
 #pragma unroll
   for (int c = 0; c < C; ++c) {

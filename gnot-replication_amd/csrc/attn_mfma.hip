@@ -392,6 +392,7 @@ hipError_t launch_mfma(const AttnApplyArgs& a, hipStream_t s) {
 
 // returns hipErrorNotSupported when the head width / LDS size has no MFMA variant (caller falls back)
 hipError_t launch_attn_apply_mfma(const AttnApplyArgs& a, bool bwd, hipStream_t s) {
+  if (a.dhr != 0 && a.dhr != a.dh) return hipErrorNotSupported;   // padded heads: the VALU forms
   if (a.nchunks <= 0) return hipSuccess;
   switch (a.dh) {
     case 16: if (mfma_ok<16>(a, bwd)) return bwd ? launch_mfma<16, true>(a, s) : launch_mfma<16, false>(a, s); break;

@@ -92,6 +92,15 @@ struct gnot_plan {
   // packed images, pad columns of the feature softmax zeroed); parameters and gradients have Dr.
   int Dr = 0;
   bool padded() const { return Dr != D; }
+  // padded heads (a head width Dr / H that is not a multiple of 4, d <= 192): the attention runs heads of
+  // dh = the next multiple of 4 (q / k / v projections place head h's rows at h * dh, the feature softmax
+  // masks the pad features, pack.hip PackJob::hr / hp), while the scramble rows (model.py:81-83) keep the
+  // real head width dhr = Dr / H.  dhr == dh otherwise
+  int dhr = 0;
+  bool head_padded() const { return dhr != dh; }
+  int hd() const { return H * dh; }                 // attention feature columns (<= D)
+  // the projections' feature-softmax pad columns: features past the H heads of dh are written as 0
+  int attn_dreal() const { return hd() < D ? hd() : 0; }
   int in = 0, th = 0, F = 0, out = 0;
   std::vector<int> lin_o, lin_i;   // out / in features per canonical Linear
   std::vector<const float*> W, b;
@@ -239,7 +248,8 @@ struct gnot_plan {
     return moe_recompute ? std::string("mrsave") : "b" + std::to_string(l) + (m1 ? ".m1save" : ".m2save");
   }
   std::vector<CopySeg> xsend, xrecv;       // scramble all-to-all: hm -> send buffer, recv buffer -> tokens
-  std::vector<int> xsend_prefix, xrecv_prefix;   // float4 prefix sums for the copy kernel
+  std::vector<int> xsend_prefix, xrecv_prefix;   // prefix sums in copy units (xunit floats) for the copy kernel
+  int xunit = 4;                                  // 4 (float4 runs), 1 with padded heads (runs of dhr floats)
   std::vector<int64_t> xsend_counts, xrecv_counts;
   CopySeg* d_xsend = nullptr;
   CopySeg* d_xrecv = nullptr;
@@ -312,23 +322,32 @@ extern "C" int gnot_plan_create(const gnot_config* cfg, gnot_plan** out) {
   const int Dr = c.n_attn_hidden_dim;
   if (c.n_head <= 0 || Dr <= 0 || Dr % c.n_head != 0)
     return fail(GNOT_E_INVALID, "n_embed should be divisible by head");   // model.py:41
-  const int dh = Dr / c.n_head;
+  const int dhr = Dr / c.n_head;
+  // the attention passes take head widths that are a multiple of 4 (4-aligned lane slices, attn.hip); any
+  // other runs on heads padded to the next multiple of 4 (gnot_plan::head_padded), at d <= 192
+  const int dh = (dhr + 3) / 4 * 4;
   // chain.hip / linear.hip run any multiple of 16 up to 192 (whole 16-wide MFMA tiles, activations in
   // registers), chain2.hip / linear2.hip d = 256; the attention passes any head width that is a multiple
   // of 4 up to 64 (4-aligned lane slices, attn.hip; the fp32-MFMA forms at 16 / 32 / 64).  A width below
   // 192 that is not a multiple of 16 runs padded to the next multiple, one in (192, 256) padded to 256
-  // (Dr real columns + zero pads)
+  // (Dr real columns + zero pads); padded heads need H * dh columns
   int D = Dr;
   if (Dr % 16 != 0 && Dr < 192) D = (Dr + 15) / 16 * 16;
   else if (Dr > 192 && Dr < 256) D = 256;            // chain2.hip / linear2.hip with pad columns
   else if (Dr > 256) D = (Dr + 63) / 64 * 64;         // 320 .. 512: chainw.hip (one Linear at a time)
+  if (dh != dhr) {
+    D = std::max(D, (c.n_head * dh + 15) / 16 * 16);
+    if (D > 192)
+      return fail(GNOT_E_INVALID, "a head width d/n_head that is not a multiple of 4 runs (on heads padded to "
+                                  "one) up to an internal width of 192 on the MI355X kernels");
+  }
   if (!((D % 16 == 0 && D >= 16 && D <= 192) || D == 256 || (D > 256 && D <= 512)))
     return fail(GNOT_E_INVALID, "hidden width must be at most 512 on the MI355X kernels");
   if (D > 256 && 64 % dh != 0)
     return fail(GNOT_E_INVALID, "above hidden width 256 the head width must divide 64 on the MI355X kernels");
   // the VALU attention-state kernel (state.hip state_partial) gives each of its 256 threads at most
   // kMaxBlk = 4 of the H (dh/4)^2 = d dh / 16 output blocks: always true up to d = 256 (d dh <= 16384)
-  if (Dr * dh > 16384)
+  if (c.n_head * dh * dh > 16384)
     return fail(GNOT_E_INVALID, "d * (d / n_head) must be at most 16384 on the MI355X kernels (attention states)");
   if (dh % 4 != 0 || dh > 64)
     return fail(GNOT_E_INVALID, "head width d/n_head must be a multiple of 4 up to 64 on the MI355X kernels");
@@ -346,7 +365,7 @@ extern "C" int gnot_plan_create(const gnot_config* cfg, gnot_plan** out) {
     return fail(GNOT_E_INVALID, "input/output widths must be in [1, hidden width]");
   gnot_plan* p = new gnot_plan();
   p->c = c;
-  p->D = D; p->Dr = Dr; p->H = c.n_head; p->dh = dh; p->E = c.n_expert; p->L = c.n_attn_layers;
+  p->D = D; p->Dr = Dr; p->H = c.n_head; p->dh = dh; p->dhr = dhr; p->E = c.n_expert; p->L = c.n_attn_layers;
   p->I = c.n_input_functions; p->KI = std::max(p->I, 1); p->DT = D / 16;
   p->NL = std::max(c.n_mlp_num_layers, 1) + 1;   // MLP(nl) has max(nl,1)+1 Linears (model.py:9-14)
   p->in = c.input_dim; p->th = c.theta_dim; p->F = c.input_func_dim; p->out = c.out_dim;
@@ -485,11 +504,18 @@ static void plan_images(gnot_plan* p) {
     return o;
   };
   // job: linear li into image im at tile offsets (o0, t0); transposed flag; bias destination
-  auto job = [&](int li, const Img& im, int o0, int t0, int OTp, int KTp, int tr, long bias_off, int x6 = 0) {
+  // heads: a q / k / v projection (padded heads: its rows placed in heads of dh, PackJob::hr / hp)
+  auto job = [&](int li, const Img& im, int o0, int t0, int OTp, int KTp, int tr, long bias_off, int x6 = 0,
+                 bool heads = false) {
     PackJob J{};
     J.x6 = x6;
     J.out = p->lin_o[li];
     J.in = p->lin_i[li];
+    if (heads && p->head_padded()) {
+      J.hr = p->dhr;
+      J.hp = p->dh;
+      J.out = p->hd();
+    }
     J.transposed = tr;
     J.o0 = o0; J.t0 = t0; J.ktot = im.KT; J.otot = im.OT;
     J.OTp = OTp; J.KTp = KTp;
@@ -545,18 +571,18 @@ static void plan_images(gnot_plan* p) {
     if (selftype) {
       A.qkv = img(3 * DT, DT);
       A.bqkv = new_bias(3 * D);
-      job(iq, A.qkv, 0, 0, DT, DT, 0, (long)A.bqkv, x6);
-      job(ik[0], A.qkv, DT, 0, DT, DT, 0, (long)(A.bqkv + D), x6);
-      job(iv[0], A.qkv, 2 * DT, 0, DT, DT, 0, (long)(A.bqkv + 2 * D), x6);
+      job(iq, A.qkv, 0, 0, DT, DT, 0, (long)A.bqkv, x6, true);
+      job(ik[0], A.qkv, DT, 0, DT, DT, 0, (long)(A.bqkv + D), x6, true);
+      job(iv[0], A.qkv, 2 * DT, 0, DT, DT, 0, (long)(A.bqkv + 2 * D), x6, true);
     } else {
       A.q = img(DT, DT);
       A.bq = new_bias(D);
-      job(iq, A.q, 0, 0, DT, DT, 0, (long)A.bq, x6);
+      job(iq, A.q, 0, 0, DT, DT, 0, (long)A.bq, x6, true);
       for (size_t i = 0; i < ik.size(); ++i) {
         Img kv = new_img(2 * DT, DT);
         const size_t bkv = new_bias(2 * D);
-        job(ik[i], kv, 0, 0, DT, DT, 0, (long)bkv);
-        job(iv[i], kv, DT, 0, DT, DT, 0, (long)(bkv + D));
+        job(ik[i], kv, 0, 0, DT, DT, 0, (long)bkv, 0, true);
+        job(iv[i], kv, DT, 0, DT, DT, 0, (long)(bkv + D), 0, true);
         A.kv.push_back(kv);
         A.bkv.push_back(bkv);
       }
@@ -568,14 +594,14 @@ static void plan_images(gnot_plan* p) {
     if (selftype) { mine.push_back(ik[0]); mine.push_back(iv[0]); }
     for (int li : mine) {
       Img t = img(DT, DT);
-      job(li, t, 0, 0, DT, DT, 1, -1, x6);
+      job(li, t, 0, 0, DT, DT, 1, -1, x6, li != io);
       p->T_img[li] = t;
     }
     if (!selftype)                          // input-function keys/values: batched fp32 kernel
       for (size_t i = 0; i < ik.size(); ++i)
         for (int li : {ik[i], iv[i]}) {
           Img t = new_img(DT, DT);
-          job(li, t, 0, 0, DT, DT, 1, -1);
+          job(li, t, 0, 0, DT, DT, 1, -1, 0, true);
           p->T_img[li] = t;
         }
   };
@@ -748,6 +774,26 @@ static void build_groups(gnot_plan* p) {
     G.jobs.push_back(J);
     G.lins.push_back(li);
   };
+  // a q / k / v projection's gradients: dz in heads of dh; padded heads: one job per head (its dhr real
+  // rows of the canonical dW / db)
+  auto lin_job_heads = [&](WgradGroup& G, int li, const float* dz, long lddz, const float* x, long ldx, long rows) {
+    if (!p->head_padded()) {
+      lin_job(G, li, dz, lddz, x, ldx, 0, rows);
+      return;
+    }
+    float* grads = p->P_("grads");
+    const int in = p->lin_i[li];
+    for (int h = 0; h < p->H; ++h) {
+      WgradJob J{};
+      J.dz = dz ? dz + (long)h * dh : nullptr; J.lddz = lddz; J.x = x; J.ldx = ldx; J.x_gelu = 0;
+      J.out = p->dhr; J.in = in;
+      J.dW = grads + p->grad_off[2 * li] + (long)h * p->dhr * in;
+      J.db = grads + p->grad_off[2 * li + 1] + (long)h * p->dhr;
+      J.P = (int)rows;
+      G.jobs.push_back(J);
+    }
+    G.lins.push_back(li);
+  };
   // chain c of a group: Linear j reads dZ_j from dz[(c*NL + j)*rows*D] and its input from the
   // chain input (j = 0) or gelu(saved pre-activation j-1)
   auto chain_group = [&](WgradGroup& G, int kcall, const std::vector<int>& firsts, long rows, const float* x0,
@@ -780,7 +826,7 @@ static void build_groups(gnot_plan* p) {
       WgradJob J{};
       J.dz = A + off[b] * lda; J.lddz = lda;
       J.x = Bm + off[b] * ldb; J.ldx = ldb;
-      J.out = p->Dr; J.in = p->Dr;                // H heads of dh (the real width)
+      J.out = p->hd(); J.in = p->hd();            // H heads of dh (the internal head width)
       J.dW = state + b * per_state;
       J.db = J.dW;
       J.w = w ? w + off[b] * ldw : nullptr; J.ldw = ldw; J.wdh = dh;
@@ -827,7 +873,7 @@ static void build_groups(gnot_plan* p) {
           WgradJob J{};
           const long o = p->fnoff[i][b];
           J.dz = kv + o * 2 * D; J.lddz = 2 * D; J.x = kv + D + o * 2 * D; J.ldx = 2 * D;
-          J.out = p->Dr; J.in = p->Dr; J.dW = st + b * per_state; J.db = J.dW; J.wdh = dh;
+          J.out = p->hd(); J.in = p->hd(); J.dW = st + b * per_state; J.db = J.dW; J.wdh = dh;
           J.state_dh = dh; J.diag_only = 1; J.P = (int)(p->fnoff[i][b + 1] - o);
           p->st_fn.jobs.push_back(J);
         }
@@ -842,8 +888,8 @@ static void build_groups(gnot_plan* p) {
       for (int i = 0; i < I; ++i) {
         float* dkv = p->P_(p->dkv_buf(l, i));
         const float* enc = p->P_("fnenc" + std::to_string(i));
-        lin_job(p->wg_fnkv, p->lin_ck(l, i), dkv, 2 * D, enc, D, 0, p->Q[i]);
-        lin_job(p->wg_fnkv, p->lin_cv(l, i), dkv + D, 2 * D, enc, D, 0, p->Q[i]);
+        lin_job_heads(p->wg_fnkv, p->lin_ck(l, i), dkv, 2 * D, enc, D, p->Q[i]);
+        lin_job_heads(p->wg_fnkv, p->lin_cv(l, i), dkv + D, 2 * D, enc, D, p->Q[i]);
       }
     finish_group(p, p->wg_fnkv);
   }
@@ -873,9 +919,9 @@ static void build_groups(gnot_plan* p) {
       WgradGroup& G = p->wg_self[l];
       const float* q1 = p->P_(s + "query1");
       lin_job(G, p->lin_so(l), dsum, D, p->P_(s + "sres"), p->Dr, 0, P);
-      lin_job(G, p->lin_sq(l), dqkv, 3 * D, q1, D, 0, P);
-      lin_job(G, p->lin_sk(l), dqkv + D, 3 * D, q1, D, 0, P);
-      lin_job(G, p->lin_sv(l), dqkv + 2 * D, 3 * D, q1, D, 0, P);
+      lin_job_heads(G, p->lin_sq(l), dqkv, 3 * D, q1, D, P);
+      lin_job_heads(G, p->lin_sk(l), dqkv + D, 3 * D, q1, D, P);
+      lin_job_heads(G, p->lin_sv(l), dqkv + 2 * D, 3 * D, q1, D, P);
       finish_group(p, G);
     }
     {
@@ -885,11 +931,11 @@ static void build_groups(gnot_plan* p) {
       const float* qin = p->P_(p->block_query(l));
       lin_job(G, p->lin_co(l), dsum, D, p->P_(s + "cres"), p->Dr, 0, P);
       if (I > 0) {
-        lin_job(G, p->lin_cq(l), dqkv, D, qin, D, 0, P);   // key/value grads: wg_fnkv
+        lin_job_heads(G, p->lin_cq(l), dqkv, D, qin, D, P);   // key/value grads: wg_fnkv
       } else {
-        lin_job(G, p->lin_cq(l), dqkv, 3 * D, qin, D, 0, P);
-        lin_job(G, p->lin_ck(l, 0), dqkv + D, 3 * D, qin, D, 0, P);
-        lin_job(G, p->lin_cv(l, 0), dqkv + 2 * D, 3 * D, qin, D, 0, P);
+        lin_job_heads(G, p->lin_cq(l), dqkv, 3 * D, qin, D, P);
+        lin_job_heads(G, p->lin_ck(l, 0), dqkv + D, 3 * D, qin, D, P);
+        lin_job_heads(G, p->lin_cv(l, 0), dqkv + 2 * D, 3 * D, qin, D, P);
       }
       finish_group(p, G);
     }
@@ -912,7 +958,8 @@ static void build_attn_tables(gnot_plan* p) {
       LinearArgs a{};
       a.nseg = 1; a.X[0] = p->P_("fnenc" + si); a.ldx = D; a.Wp[0] = A.kv[i].p; a.nsum = 1; a.K = D;
       a.bias = pbias + A.bkv[i]; a.Y = p->P_(s + "ckv" + si); a.ldy = 2 * D; a.NO = 2 * D; a.P = (int)p->Q[i];
-      a.epi = EPI_STORE; a.nsoft = D; a.dh = p->dh; a.dreal = p->padded() ? p->Dr : 0;
+      a.epi = EPI_STORE; a.nsoft = D; a.dh = p->dh; a.dreal = p->attn_dreal();
+      a.dhr = p->head_padded() ? p->dhr : 0;
       p->fwd_kv_jobs.push_back(a);
     }
   if (!p->training) return;
@@ -1006,12 +1053,12 @@ static void build_exchange(int B, const std::vector<long>& nglob, int H, int dh,
       }
 }
 
-static std::vector<int> seg_prefix4(const std::vector<CopySeg>& segs) {
+static std::vector<int> seg_prefix(const std::vector<CopySeg>& segs, int unit) {
   std::vector<int> pre;
   int acc = 0;
   for (const auto& sg : segs) {
     pre.push_back(acc);
-    acc += (int)(sg.len / 4);
+    acc += (int)(sg.len / unit);
   }
   pre.push_back(acc);
   return pre;
@@ -1143,10 +1190,12 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
       if (p->xoff[b + 1] - p->xoff[b] != hi - lo)
         return fail(GNOT_E_INVALID, "x_off does not match this rank's shard of n_global (gnot_shard_range)");
     }
-    build_exchange(B, p->nglob, p->H, p->dh, p->rank, p->world, p->xsend, p->xrecv, p->xsend_counts,
+    build_exchange(B, p->nglob, p->H, p->dhr, p->rank, p->world, p->xsend, p->xrecv, p->xsend_counts,
                    p->xrecv_counts);
-    p->xsend_prefix = seg_prefix4(p->xsend);
-    p->xrecv_prefix = seg_prefix4(p->xrecv);
+    // the runs are multiples of the real head width (offsets too): float4 copies unless it is not a multiple of 4
+    p->xunit = p->dhr % 4 == 0 ? 4 : 1;
+    p->xsend_prefix = seg_prefix(p->xsend, p->xunit);
+    p->xrecv_prefix = seg_prefix(p->xrecv, p->xunit);
   } else {
     p->xsend.clear(); p->xrecv.clear(); p->xsend_prefix.clear(); p->xrecv_prefix.clear();
   }
@@ -1549,7 +1598,8 @@ int run_linear(Ctx& c, const float* X, long ldx, int K, const Img& A, const floa
   a.nseg = 1; a.X[0] = X; a.Wp[0] = A.p; a.ldx = ldx; a.nsum = 1; a.sum_stride = 0; a.K = K;
   a.bias = bias; a.Y = Y; a.ldy = ldy; a.NO = NO; a.P = (int)P;
   a.epi = epi; a.nsoft = nsoft; a.dh = c.p->dh; a.np = c.p->npk(); a.img = c.p->lin_img();
-  a.dreal = (nsoft > 0 && c.p->padded()) ? c.p->Dr : 0;
+  a.dreal = nsoft > 0 ? c.p->attn_dreal() : 0;
+  a.dhr = (nsoft > 0 && c.p->head_padded()) ? c.p->dhr : 0;
   a.ncol = ncol;
   GNOT_CK(c.p->D == 256 ? launch_linear2(a, c.s) : launch_linear(a, c.p->D, c.s));
   return GNOT_OK;
@@ -1741,15 +1791,15 @@ int shard_exchange(Ctx& c, float* hm, float* tok, bool reverse) {
   float* xb = p->P_("xb");
   const int ns = (int)p->xsend.size(), nr = (int)p->xrecv.size();
   if (!reverse) {
-    GNOT_CK(launch_segcopy(p->d_xsend, p->d_xsend_prefix, ns, p->xsend_prefix.back(), hm, xa, false, c.s));
+    GNOT_CK(launch_segcopy(p->d_xsend, p->d_xsend_prefix, ns, p->xsend_prefix.back(), hm, xa, false, c.s, p->xunit));
     if (p->comm.alltoallv(p->comm.user, xa, p->xsend_counts.data(), xb, p->xrecv_counts.data(), c.s) != 0)
       return fail(GNOT_E_HIP, "gnot_comm.alltoallv failed");
-    GNOT_CK(launch_segcopy(p->d_xrecv, p->d_xrecv_prefix, nr, p->xrecv_prefix.back(), xb, tok, false, c.s));
+    GNOT_CK(launch_segcopy(p->d_xrecv, p->d_xrecv_prefix, nr, p->xrecv_prefix.back(), xb, tok, false, c.s, p->xunit));
   } else {
-    GNOT_CK(launch_segcopy(p->d_xrecv, p->d_xrecv_prefix, nr, p->xrecv_prefix.back(), tok, xb, true, c.s));
+    GNOT_CK(launch_segcopy(p->d_xrecv, p->d_xrecv_prefix, nr, p->xrecv_prefix.back(), tok, xb, true, c.s, p->xunit));
     if (p->comm.alltoallv(p->comm.user, xb, p->xrecv_counts.data(), xa, p->xsend_counts.data(), c.s) != 0)
       return fail(GNOT_E_HIP, "gnot_comm.alltoallv failed");
-    GNOT_CK(launch_segcopy(p->d_xsend, p->d_xsend_prefix, ns, p->xsend_prefix.back(), xa, hm, true, c.s));
+    GNOT_CK(launch_segcopy(p->d_xsend, p->d_xsend_prefix, ns, p->xsend_prefix.back(), xa, hm, true, c.s, p->xunit));
   }
   return GNOT_OK;
 }
@@ -1772,6 +1822,7 @@ int attn_forward(Ctx& c, int l, bool cross, const float* q_in, float* res_out, f
     for (int i = 0; i < p->I; ++i) ap.state[i] = p->P_(s + "cstate" + std::to_string(i));
     ap.q = q; ap.ldq = D; ap.nsrc = p->I; ap.chunks = p->d_qchunks; ap.nchunks = nq; ap.off = p->d_xoff;
     ap.H = p->H; ap.dh = p->dh; ap.res = p->sharded ? p->P_("xb") : res_out;
+    ap.dhr = p->head_padded() ? p->dhr : 0;
     GNOT_CK(launch_attn_apply_fwd(ap, c.s));
   } else {
     float* qkv = p->P_(cross ? s + "cq" : s + "sq");
@@ -1782,6 +1833,7 @@ int attn_forward(Ctx& c, int l, bool cross, const float* q_in, float* res_out, f
     AttnApplyArgs ap{};
     ap.q = qkv; ap.ldq = 3 * D; ap.nsrc = 1; ap.state[0] = st; ap.chunks = p->d_qchunks; ap.nchunks = nq;
     ap.off = p->d_xoff; ap.H = p->H; ap.dh = p->dh; ap.res = p->sharded ? p->P_("xb") : res_out;
+    ap.dhr = p->head_padded() ? p->dhr : 0;
     GNOT_CK(launch_attn_apply_fwd(ap, c.s));
   }
   if (p->sharded) GNOT_RUN(shard_exchange(c, p->P_("xb"), res_out, false));   // the scramble, across ranks
@@ -1817,6 +1869,7 @@ int attn_backward(Ctx& c, int l, bool cross) {
     AttnApplyArgs ap{};
     ap.q = q; ap.ldq = D; ap.nsrc = p->I; ap.chunks = p->d_qchunks; ap.nchunks = nq; ap.off = p->d_xoff;
     ap.H = p->H; ap.dh = p->dh; ap.dres = dres; ap.dq_pre = dqkv; ap.lddq = D; ap.lddu = D;
+    ap.dhr = p->head_padded() ? p->dhr : 0;
     for (int i = 0; i < p->I; ++i) {
       const std::string si = std::to_string(i);
       ap.state[i] = p->P_(s + "cstate" + si);
@@ -1837,6 +1890,7 @@ int attn_backward(Ctx& c, int l, bool cross) {
     ap.chunks = p->d_qchunks; ap.nchunks = nq; ap.off = p->d_xoff; ap.H = p->H; ap.dh = p->dh;
     ap.dres = dres; ap.dq_pre = dqkv; ap.lddq = 3 * D; ap.du[0] = p->P_("du0"); ap.lddu = D;
     ap.dden[0] = p->P_("dden0");
+    ap.dhr = p->head_padded() ? p->dhr : 0;
     GNOT_CK(launch_attn_apply_bwd(ap, c.s));
     float* dst = p->P_("dstate0");
     GNOT_RUN(run_state(c, cross ? p->dst_c[l][0] : p->dst_s[l]));

@@ -26,6 +26,11 @@ struct PackJob {
                        //    same output-major (chain2.hip); 3: output-major, 1 RNE bf16 piece; 4: k-major,
                        //    1 RNE bf16 piece (chain.hip in the bf16 mode); 0: fp32
   int otot;            // x6: output tiles of the whole image (its k-major block stride)
+  // padded heads (a head width d / H that is not a multiple of 4): W's rows come in H heads of hr real rows,
+  // the image holds them in heads of hp >= hr (row h * hp + j <- W row h * hr + j, j < hr; the rest zero).
+  // out is then H * hp.  Applies to the image rows (forward) or the contraction index (transposed) and to
+  // the bias copy.  0: rows map 1:1
+  int hr = 0, hp = 0;
 };
 // pack tiles of a job: fp32 images have OTp*KTp tiles, x6 images OTp*ceil(KTp/2) blocks
 inline int pack_tiles(const PackJob& J) { return J.x6 ? J.OTp * ((J.KTp + 1) / 2) : J.OTp * J.KTp; }
@@ -59,6 +64,9 @@ struct LinearArgs {
   // output column c with c % D >= dreal is written as 0 (the softmax of a head's features must not leak
   // into the pad columns, which the next kernels read as exact zeros); 0 = no pad columns
   int dreal = 0;
+  // padded heads: heads of dh internal features of which the first dhr are real; the feature softmax
+  // excludes (and writes 0 to) the others.  0: every feature of a head is real
+  int dhr = 0;
   int ncol = 0;                      // store only output columns [0, ncol) (row pitch ldy < NO); 0 = all NO
 };
 hipError_t launch_linear(const LinearArgs& a, int D, hipStream_t s);
@@ -223,6 +231,9 @@ struct AttnApplyArgs {
   const long* off;                   // [B+1] sample offsets (device)
   int H, dh;
   float* res;                        // [P, d] head-major per sample (the scramble)
+  // padded heads: the scramble holds heads of dhr real features (element (h, n, j) at (h N_b + n) dhr + j,
+  // j < dhr), while q / states / du / dq run heads of dh (pad features zero).  0: dhr = dh
+  int dhr = 0;
   // backward
   const float* dres;                 // [P, d] head-major per sample
   float* dq_pre; long lddq;          // grad wrt pre-softmax q, point-major
@@ -266,13 +277,14 @@ hipError_t launch_add_cols(const float* a, long lda, const float* b, long ldb, i
 // out[b][t] = sum over rows [off[b], off[b+1]) of a[row][c0 + t], t < ncols (fixed order)
 hipError_t launch_seg_colsum(const float* a, long lda, int c0, int ncols, const long* off, int B, float* out,
                              hipStream_t s);
-// segmented copy: dst[seg.dst + i] = src[seg.src + i], i < seg.len (floats, multiples of 4);
-// reverse swaps the roles of src/dst offsets.  prefix4: float4 prefix sums of the lengths [nseg + 1].
+// segmented copy: dst[seg.dst + i] = src[seg.src + i], i < seg.len (floats); reverse swaps the roles of
+// src/dst offsets.  unit 4: every offset and length a multiple of 4 (float4 copies), unit 1: any.  prefix:
+// prefix sums of the lengths in units [nseg + 1], total = prefix[nseg].
 struct CopySeg {
   long a, b, len;      // a = source offset, b = destination offset (forward direction)
 };
-hipError_t launch_segcopy(const CopySeg* segs, const int* prefix4, int nseg, int total4, const float* src, float* dst,
-                          bool reverse, hipStream_t s);
+hipError_t launch_segcopy(const CopySeg* segs, const int* prefix, int nseg, int total, const float* src, float* dst,
+                          bool reverse, hipStream_t s, int unit = 4);
 
 // ------------------------------------------------------------------ training step (train.hip)
 int rel_l2_splits(const long* off_host, int B);

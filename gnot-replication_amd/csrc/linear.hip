@@ -127,7 +127,17 @@ GNOT_DEV void linear_body(const LinearArgs& a, float4* wlds) {
   }
   float h[OC][4];
   acc_to_regs<OC>(acc, h);
-  if (c * 16 * OC < a.nsoft) softmax_heads<OC>(h, a.dh, lane >> 4);
+  if (c * 16 * OC < a.nsoft) {
+    if (a.dhr > 0) {
+      // padded heads: the pad features of every head (j >= dhr) take no part in its softmax (exp -> 0)
+#pragma unroll
+      for (int T = 0; T < OC; ++T)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if ((c * 16 * OC + 16 * T + 4 * (lane >> 4) + r) % D % a.dh >= a.dhr) h[T][r] = -INFINITY;
+    }
+    softmax_heads<OC>(h, a.dh, lane >> 4);
+  }
   if (a.dreal > 0) {
     // pad columns of a padded width (D is the tile width; features dreal .. D-1 of each D-block)
 #pragma unroll

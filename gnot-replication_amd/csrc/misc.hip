@@ -104,28 +104,36 @@ hipError_t launch_moe_combine_b16(const float* base, const float* stage, long st
   return hipGetLastError();
 }
 
-__global__ void __launch_bounds__(256) segcopy_kernel(const CopySeg* __restrict__ segs, const int* __restrict__ prefix4,
-                                                      int nseg, int total4, const float* __restrict__ src,
+// U = 4: float4 units (every run offset / length a multiple of 4 floats); U = 1: single floats (padded heads:
+// runs of a head width that is not a multiple of 4)
+template <int U>
+__global__ void __launch_bounds__(256) segcopy_kernel(const CopySeg* __restrict__ segs, const int* __restrict__ prefix,
+                                                      int nseg, int total, const float* __restrict__ src,
                                                       float* __restrict__ dst, int reverse) {
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < total4; i += gridDim.x * 256) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
     int lo = 0, hi = nseg - 1;
     while (lo < hi) {
       const int mid = (lo + hi + 1) >> 1;
-      if (prefix4[mid] <= i) lo = mid; else hi = mid - 1;
+      if (prefix[mid] <= i) lo = mid; else hi = mid - 1;
     }
     const CopySeg sg = segs[lo];
-    const long off = (long)(i - prefix4[lo]) * 4;
+    const long off = (long)(i - prefix[lo]) * U;
     const long so = reverse ? sg.b : sg.a, dof = reverse ? sg.a : sg.b;
-    *reinterpret_cast<float4*>(dst + dof + off) = *reinterpret_cast<const float4*>(src + so + off);
+    if constexpr (U == 4) *reinterpret_cast<float4*>(dst + dof + off) = *reinterpret_cast<const float4*>(src + so + off);
+    else dst[dof + off] = src[so + off];
   }
 }
 
-hipError_t launch_segcopy(const CopySeg* segs, const int* prefix4, int nseg, int total4, const float* src, float* dst,
-                          bool reverse, hipStream_t s) {
-  if (nseg <= 0 || total4 <= 0) return hipSuccess;
-  const int blocks = std::min((total4 + 255) / 256, 4096);
-  hipLaunchKernelGGL(segcopy_kernel, dim3(blocks), dim3(256), 0, s, segs, prefix4, nseg, total4, src, dst,
-                     reverse ? 1 : 0);
+hipError_t launch_segcopy(const CopySeg* segs, const int* prefix, int nseg, int total, const float* src, float* dst,
+                          bool reverse, hipStream_t s, int unit) {
+  if (nseg <= 0 || total <= 0) return hipSuccess;
+  const int blocks = std::min((total + 255) / 256, 4096);
+  if (unit == 4)
+    hipLaunchKernelGGL(segcopy_kernel<4>, dim3(blocks), dim3(256), 0, s, segs, prefix, nseg, total, src, dst, reverse ? 1 : 0);
+  else if (unit == 1)
+    hipLaunchKernelGGL(segcopy_kernel<1>, dim3(blocks), dim3(256), 0, s, segs, prefix, nseg, total, src, dst, reverse ? 1 : 0);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

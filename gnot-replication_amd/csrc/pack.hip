@@ -13,6 +13,14 @@
 
 namespace gnot {
 
+// W row of image row / contraction index i (padded heads: PackJob::hr / hp), or -1 for a zero row
+GNOT_DEV int pack_row(const PackJob& J, int i) {
+  if (i >= J.out) return -1;
+  if (J.hp == 0) return i;
+  const int h = i / J.hp, j = i - h * J.hp;
+  return j < J.hr ? h * J.hr + j : -1;
+}
+
 // one wave per (job, tile)
 __global__ void __launch_bounds__(64) pack_kernel(const PackJob* __restrict__ jobs,
                                                   const int* __restrict__ prefix, int njobs) {
@@ -40,8 +48,13 @@ __global__ void __launch_bounds__(64) pack_kernel(const PackJob* __restrict__ jo
       const int f = 32 * kb + (j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4));   // contraction index
       const int row = 16 * o + r16;
       float v = 0.f;
-      if (!J.transposed) v = (row < J.out && f < J.in) ? J.W[(long)row * J.in + f] : 0.f;
-      else v = (f < J.out && row < J.in) ? J.W[(long)f * J.in + row] : 0.f;
+      if (!J.transposed) {
+        const int wr = pack_row(J, row);
+        v = (wr >= 0 && f < J.in) ? J.W[(long)wr * J.in + f] : 0.f;
+      } else {
+        const int wr = pack_row(J, f);
+        v = (wr >= 0 && row < J.in) ? J.W[(long)wr * J.in + row] : 0.f;
+      }
       const unsigned b = __builtin_bit_cast(unsigned, v);
       const float r1 = v - __builtin_bit_cast(float, b & 0xFFFF0000u);
       const unsigned b1 = __builtin_bit_cast(unsigned, r1);
@@ -75,7 +88,10 @@ __global__ void __launch_bounds__(64) pack_kernel(const PackJob* __restrict__ jo
     }
     if (J.bias_dst && t == 0) {
       const int nb = 16 * J.OTp;
-      for (int i = lane; i < nb; i += WAVE) J.bias_dst[i] = (i < J.out && J.b) ? J.b[i] : 0.f;
+      for (int i = lane; i < nb; i += WAVE) {
+        const int br = pack_row(J, i);
+        J.bias_dst[i] = (br >= 0 && J.b) ? J.b[br] : 0.f;
+      }
     }
     return;
   }
@@ -83,26 +99,29 @@ __global__ void __launch_bounds__(64) pack_kernel(const PackJob* __restrict__ jo
   int o, T;
   if (!J.transposed) {
     o = t / J.KTp; T = t % J.KTp;
-    const int row = 16 * o + r16;
+    const int wr = pack_row(J, 16 * o + r16);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int col = 16 * T + 4 * g + r;
-      v[r] = (row < J.out && col < J.in) ? J.W[(long)row * J.in + col] : 0.f;
+      v[r] = (wr >= 0 && col < J.in) ? J.W[(long)wr * J.in + col] : 0.f;
     }
   } else {                              // contraction runs over W's rows
     o = t / J.KTp; T = t % J.KTp;
     const int col = 16 * o + r16;       // W column (input feature)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int row = 16 * T + 4 * g + r;
-      v[r] = (row < J.out && col < J.in) ? J.W[(long)row * J.in + col] : 0.f;
+      const int wr = pack_row(J, 16 * T + 4 * g + r);
+      v[r] = (wr >= 0 && col < J.in) ? J.W[(long)wr * J.in + col] : 0.f;
     }
   }
   J.dst[((long)(J.o0 + o) * J.ktot + J.t0 + T) * WAVE + lane] = make_float4(v[0], v[1], v[2], v[3]);
   // padded bias copy, done by the job's first tile
   if (J.bias_dst && t == 0) {
     const int nb = 16 * J.OTp;
-    for (int i = lane; i < nb; i += WAVE) J.bias_dst[i] = (i < J.out && J.b) ? J.b[i] : 0.f;
+    for (int i = lane; i < nb; i += WAVE) {
+      const int br = pack_row(J, i);
+      J.bias_dst[i] = (br >= 0 && J.b) ? J.b[br] : 0.f;
+    }
   }
 }
 

@@ -124,6 +124,10 @@ def test_point_sharded_gnot_matches_oracle(world, case):
     (3, dict(cfg=dict(input_dim=3, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=1, d=208,
                       n_mlp_num_layers=2, n_expert=2, n_head=13, n_input_functions=0),
              Ns=[131, 40], Ms=[])),
+    # padded HEADS: 4 heads of 25 (run as heads of 28; the scramble exchange at the real head width)
+    (2, dict(cfg=dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=2, n_attn_layers=1, d=100,
+                      n_mlp_num_layers=2, n_expert=2, n_head=4, n_input_functions=1),
+             Ns=[121, 66], Ms=[[33, 20]])),
 ])
 def test_point_sharded_padded_widths(world, case):
     _run_sharded_case(world, case)

@@ -2,9 +2,10 @@
 n_head (model.py:41).  This core takes every hidden width d up to 192 (the chain.hip / linear.hip
 kernels, whole 16-wide MFMA tiles; a d that is not a multiple of 16 runs padded to the next one with
 exact-zero pad columns) and d = 256 (chain2.hip / linear2.hip; d in (192, 256) padded to it), with
-any head width dh = d / H that is a multiple of 4 up to 64 (the attention passes split a head into
-4-aligned lane slices; the projections' feature softmax reduces a head that straddles 16-feature tiles
-across the 4 lane groups of a point, gnot_common.h softmax_heads).
+any head width dh = d / H up to 64 (the attention passes split a head into 4-aligned lane slices; the
+projections' feature softmax reduces a head that straddles 16-feature tiles across the 4 lane groups of a
+point, gnot_common.h softmax_heads; a head width that is not a multiple of 4 runs on heads padded to one,
+up to an internal width of 192).
 
 Each case is checked against the float64 oracle (oracle/gnot_oracle.py, pinned to the reference's
 fixtures) at north_star's 1e-4: output and every parameter gradient (golden_util.check_parity), on a
@@ -44,6 +45,14 @@ CASES = {
     "d60_h15": _cfg(60, 15, 2, 0),        # dh 4, kernels at d = 64, self-attention (fused q|k|v) only
     "d208_h13": _cfg(208, 13, 2, 1),      # dh 16, the d = 256 kernels (chain2 / linear2 / wide wgrad) padded
     "d224_h7": _cfg(224, 7, 3, 0),        # dh 32, d = 256 kernels, self-attention only
+    # head widths that are not a multiple of 4 run on heads padded to one (engine.cpp gnot_plan::head_padded:
+    # q / k / v rows at h * dh', the feature softmax masked to the real features, the scramble at the real
+    # head width, per-head weight-gradient jobs)
+    "d100_h4": _cfg(100, 4, 2, 1),        # dh 25 -> 28, kernels at d = 112, batched input-function K/V
+    "d90_h6": _cfg(90, 6, 2, 0, L=2),     # dh 15 -> 16, kernels at d = 96, fused q|k|v in both attentions
+    "d30_h2": _cfg(30, 2, 2, 2),          # dh 15 -> 16, kernels at d = 32, two input functions
+    "d21_h7": _cfg(21, 7, 2, 0),          # dh 3 -> 4, kernels at d = 32
+    "d150_h6": _cfg(150, 6, 2, 1),        # dh 25 -> 28: H dh' = 168 > 160, kernels at d = 176
     # d > 256: the chains one Linear at a time (chainw.hip) on the fp32-MFMA projection kernel
     "d320_h10": _cfg(320, 10, 2, 1),      # dh 32 (d * dh <= 16384: the VALU state kernel's block budget)
     "d288_h18": _cfg(288, 18, 3, 0, nl=2),  # dh 16, padded to 320, self-attention only
@@ -104,7 +113,7 @@ def test_wide_io_widths_above_256():
     assert not errs, errs
 
 
-@pytest.mark.parametrize("name", ["d100_h5", "d208_h13", "d288_h18"])
+@pytest.mark.parametrize("name", ["d100_h5", "d208_h13", "d288_h18", "d100_h4"])
 def test_padded_width_pad_columns_stay_zero_across_steps(name):
     """Padded widths keep their pad columns at exact zero only because the workspace is cleared at bind
     and no kernel writes a non-zero pad value.  Three steps on one bound plan: the
@@ -125,7 +134,7 @@ def test_padded_width_pad_columns_stay_zero_across_steps(name):
     torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("name", ["d16_h4", "d96_h8", "d100_h5", "d144_h4", "d176_h4", "d192_h6"])
+@pytest.mark.parametrize("name", ["d16_h4", "d96_h8", "d100_h5", "d144_h4", "d176_h4", "d192_h6", "d100_h4", "d90_h6"])
 def test_width_bf16_mode(name):
     """The bf16 arithmetic mode at d <= 192 (chain.hip / linear.hip / the 128-tile weight gradients on one
     RNE bf16 piece per operand), padded widths included: north_star's 1e-2 norm-wise vs the fp64 oracle, and
