@@ -126,8 +126,16 @@ chain_fwd_kernel(ChainArgs a) {
 
 // NP = 3: exact fp32 MFMA on fp32 fragment images of W^T; NP = 1 (bf16 mode): one RNE bf16 piece per
 // operand on k-major one-piece images of W^T (pack x6 = 4), fp32 accumulation
+// three waves per SIMD at d <= 128 (as the forward): 162-165 VGPRs without spills at d = 128, where the
+// compiler's own choice (132 VGPRs + 48 AGPRs) allowed two, so a configs[1] launch (2,500 waves) ran in two
+// rounds.  d = 112 would spill at three.  -DGNOT_CHAIN_BWD_OCC=1 builds the compiler's choice (A/B)
+#ifndef GNOT_CHAIN_BWD_OCC
+#define GNOT_CHAIN_BWD_OCC 3
+#endif
 template <int D, int KT0, int OTL, int NP>
-__global__ void __launch_bounds__(64 * kChainWaves) chain_bwd_kernel(ChainArgs a) {
+__global__ void __launch_bounds__(64 * kChainWaves)
+__attribute__((amdgpu_waves_per_eu((D <= 128 && D != 112) ? GNOT_CHAIN_BWD_OCC : 1)))
+chain_bwd_kernel(ChainArgs a) {
   constexpr int DT = D / 16;
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4;
