@@ -10,6 +10,9 @@
 //                      first nsoft columns).
 //   linear2_seg_kernel several K-segments (NO = 256): the 16 output tiles accumulate in registers
 //                      across the segments, one segment's input split at a time.
+#include <algorithm>
+#include <cstdlib>
+
 #include "gnot_kernels.h"
 #include "x6_core.h"
 
@@ -30,11 +33,14 @@ __global__ void __launch_bounds__(64 * l2_waves<NP>(), 2) linear2_kernel(LinearA
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
   const long p = ((long)blockIdx.x * l2_waves<NP>() + wave) * 16 + (lane & 15);
   const bool valid = p < a.P;
-  const int OT = a.NO / 16;
+  // output tiles [ob, oe) of this workgroup: grid.y splits the NO / 16 tiles into equal chunks of whole
+  // head groups (small batches: more workgroups than points / 16 / waves alone give, launch_linear2_np)
+  const int OTc = a.NO / 16 / (int)gridDim.y;
+  const int ob = (int)blockIdx.y * OTc, oe = ob + OTc;
   const u32x4* W = reinterpret_cast<const u32x4*>(a.Wp[0]);
   C2Stream st{c2lds, c2_tile_u4(KB, NP), 0, wave, lane, l2_waves<NP>()};
-  stage_image(reinterpret_cast<float4*>(c2lds), reinterpret_cast<const float4*>(W), c2_tile_u4(KB, NP), l2_waves<NP>(),
-              wave, lane);
+  stage_image(reinterpret_cast<float4*>(c2lds), reinterpret_cast<const float4*>(W + (size_t)ob * c2_tile_u4(KB, NP)),
+              c2_tile_u4(KB, NP), l2_waves<NP>(), wave, lane);
   u32x4 bp[KB][NP];
   {
     float x[DT][4];
@@ -45,22 +51,22 @@ __global__ void __launch_bounds__(64 * l2_waves<NP>(), 2) linear2_kernel(LinearA
   // the MFMAs: a load placed after a barrier would expose its full latency on every tile
   float4 bn[TPH];
 #pragma unroll
-  for (int k = 0; k < TPH; ++k) bn[k] = a.bias ? ld4(a.bias + 16 * k + 4 * g) : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int k = 0; k < TPH; ++k) bn[k] = a.bias ? ld4(a.bias + 16 * (ob + k) + 4 * g) : make_float4(0.f, 0.f, 0.f, 0.f);
   const long pc = valid ? p : 0;
-  for (int o0 = 0; o0 < OT; o0 += TPH) {
+  for (int o0 = ob; o0 < oe; o0 += TPH) {
     float h[TPH][4];
     float4 bc[TPH], old[TPH];
 #pragma unroll
     for (int k = 0; k < TPH; ++k) {
       bc[k] = bn[k];
-      if (a.bias && o0 + TPH < OT) bn[k] = ld4(a.bias + 16 * (o0 + TPH + k) + 4 * g);
+      if (a.bias && o0 + TPH < oe) bn[k] = ld4(a.bias + 16 * (o0 + TPH + k) + 4 * g);
       if (a.epi == EPI_ACCUM && !(a.ncol > 0 && 16 * (o0 + k) + 4 * g >= a.ncol))
         old[k] = ld4(a.Y + pc * a.ldy + 16 * (o0 + k) + 4 * g);
     }
 #pragma unroll
     for (int k = 0; k < TPH; ++k) {
       const int o = o0 + k;
-      const u32x4* cb = st.begin(W, o, OT, c2_tile_u4(KB, NP), nullptr, 0);
+      const u32x4* cb = st.begin(W, o, oe, c2_tile_u4(KB, NP), nullptr, 0);
       // the epilogue form with no epilogue: its scheduling fences keep k-block t+1's fragment reads ahead
       // of block t's MFMAs (the plain form compiled to reads issued next to their MFMAs here)
       const f32x4 acc = c2_tile_epi<KB, NP, true>(cb, bp, f32x4{bc[k].x, bc[k].y, bc[k].z, bc[k].w}, lane,
@@ -116,8 +122,12 @@ __global__ void __launch_bounds__(64 * l2_waves<NP>(), 2) linear2_seg_kernel(Lin
   const long p = ((long)blockIdx.x * l2_waves<NP>() + wave) * 16 + (lane & 15);
   const bool valid = p < a.P;
   C2Stream st{c2lds, c2_tile_u4(KB, NP), 0, wave, lane, l2_waves<NP>()};
-  stage_image(reinterpret_cast<float4*>(c2lds), reinterpret_cast<const float4*>(a.Wp[0]), c2_tile_u4(KB, NP),
-              l2_waves<NP>(), wave, lane);
+  // output tiles [ob, oe) of this workgroup (grid.y chunks, as linear2_kernel)
+  const int OTc = DT / (int)gridDim.y;
+  const int ob = (int)blockIdx.y * OTc, oe = ob + OTc;
+  constexpr int TU = c2_tile_u4(KB, NP);
+  stage_image(reinterpret_cast<float4*>(c2lds), reinterpret_cast<const float4*>(reinterpret_cast<const u32x4*>(a.Wp[0]) + (size_t)ob * TU),
+              TU, l2_waves<NP>(), wave, lane);
   f32x4 acc[DT];
 #pragma unroll
   for (int o = 0; o < DT; ++o) {
@@ -136,16 +146,18 @@ __global__ void __launch_bounds__(64 * l2_waves<NP>(), 2) linear2_seg_kernel(Lin
       c2_split<DT, NP>(x, bp);
     }
     const u32x4* W = reinterpret_cast<const u32x4*>(a.Wp[s]);
-    const u32x4* next = s + 1 < a.nseg ? reinterpret_cast<const u32x4*>(a.Wp[s + 1]) : nullptr;
+    const u32x4* next = s + 1 < a.nseg ? reinterpret_cast<const u32x4*>(a.Wp[s + 1]) + (size_t)ob * TU : nullptr;
 #pragma unroll
     for (int o = 0; o < DT; ++o) {
-      const u32x4* cb = st.begin(W, o, DT, c2_tile_u4(KB, NP), next, c2_tile_u4(KB, NP));
+      if (o < ob || o >= oe) continue;                // workgroup-uniform
+      const u32x4* cb = st.begin(W, o, oe, TU, next, TU);
       acc[o] = c2_tile_epi<KB, NP, true>(cb, bp, acc[o], lane, [](int) {});   // reads one k-block ahead
     }
   }
   if (valid) {
 #pragma unroll
     for (int o = 0; o < DT; ++o) {
+      if (o < ob || o >= oe) continue;
       float4* y = reinterpret_cast<float4*>(a.Y + p * a.ldy + 16 * o + 4 * g);
       float4 v = make_float4(acc[o][0], acc[o][1], acc[o][2], acc[o][3]);
       if (a.epi == EPI_ACCUM) {
@@ -164,10 +176,26 @@ bool linear2_supported(const LinearArgs& a, int D) {
          (a.nseg == 1 ? (a.nsoft == 0 || a.dh == 16 || a.dh == 32 || a.dh == 64) : (a.NO == 256 && a.nsoft == 0 && a.ncol == 0));
 }
 
+// output-tile chunks per launch: enough workgroups for two per CU (their register budget) on small batches
+// (configs[0]: 16,384 points = 256 workgroups of 4 waves, each streaming the whole image tile by tile, one wave
+// per SIMD); a divisor of the head groups, 1 from 512 point workgroups up (GNOT_LINEAR2_CHUNKS overrides)
+static int l2_chunks(int nwg, int groups) {
+  static const int env = [] {
+    const char* e = std::getenv("GNOT_LINEAR2_CHUNKS");
+    return e ? std::atoi(e) : 0;
+  }();
+  int want = env > 0 ? env : (512 + nwg - 1) / nwg;
+  want = std::max(1, std::min(want, groups));
+  while (groups % want) --want;
+  return want;
+}
+
 template <int NP>
 static hipError_t launch_linear2_np(const LinearArgs& a, hipStream_t s) {
   const size_t lds = 2 * (size_t)c2_tile_u4(8, NP) * 16;
-  const dim3 grid((a.P + 16 * l2_waves<NP>() - 1) / (16 * l2_waves<NP>())), block(64 * l2_waves<NP>());
+  const int nwg = (a.P + 16 * l2_waves<NP>() - 1) / (16 * l2_waves<NP>());
+  const int tph = a.nseg > 1 ? 1 : (a.nsoft ? a.dh / 16 : 2);
+  const dim3 grid(nwg, l2_chunks(nwg, a.NO / 16 / tph)), block(64 * l2_waves<NP>());
   static bool attr = false;
   if (!attr) {
     for (const void* f : {reinterpret_cast<const void*>(linear2_kernel<1, NP>), reinterpret_cast<const void*>(linear2_kernel<2, NP>),
@@ -178,7 +206,6 @@ static hipError_t launch_linear2_np(const LinearArgs& a, hipStream_t s) {
   if (a.nseg > 1) {
     hipLaunchKernelGGL(linear2_seg_kernel<NP>, grid, block, lds, s, a);
   } else {
-    const int tph = a.nsoft ? a.dh / 16 : 2;
     if (tph == 1) hipLaunchKernelGGL((linear2_kernel<1, NP>), grid, block, lds, s, a);
     else if (tph == 2) hipLaunchKernelGGL((linear2_kernel<2, NP>), grid, block, lds, s, a);
     else hipLaunchKernelGGL((linear2_kernel<4, NP>), grid, block, lds, s, a);
