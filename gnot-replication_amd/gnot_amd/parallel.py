@@ -114,6 +114,7 @@ class PointShardComm:
                 t = self._view(buf, count)
                 with self._on(stream):
                     if self.stage:
+                        _no_capture()
                         # host staging (gloo, tests): the whole device first, then blocking copies.  Under
                         # ExternalStream(0) (a rank whose current stream is the null stream) .cpu() did NOT
                         # wait for the engine's kernels: the 2-rank sharded 70k test read state buffers before
@@ -140,6 +141,7 @@ class PointShardComm:
                 s = self._view(send, sum(sc)) if sum(sc) else torch.empty(0, device=dev)
                 r = self._view(recv, sum(rc)) if sum(rc) else torch.empty(0, device=dev)
                 if self.stage:
+                    _no_capture()
                     torch.cuda.synchronize(dev)
                     hr = torch.empty(sum(rc), dtype=torch.float32)
                     dist.all_to_all_single(hr, s.cpu(), rc, sc, group=self.group)
@@ -153,6 +155,14 @@ class PointShardComm:
             return -1
 
 
+def _no_capture():
+    """The host-staged collectives block on the device and copy through host memory, which a stream
+    capture cannot record (and a device synchronize inside one invalidates the capture for the caller's
+    later eager launches): refuse cleanly, so the engine call fails and bench.py runs eager steps."""
+    if torch.cuda.is_current_stream_capturing():
+        raise RuntimeError("host-staged (gloo) collectives cannot be captured into a HIP graph")
+
+
 class _SumOverRanks(torch.autograd.Function):
     """all-reduce(sum) whose backward is the identity: every rank evaluates the SAME loss from the
     reduced sums, so d loss / d (local partial) is the gradient of the reduced value itself."""
@@ -161,6 +171,7 @@ class _SumOverRanks(torch.autograd.Function):
     def forward(ctx, t, group, stage):
         out = t.clone()
         if stage:
+            _no_capture()
             h = out.cpu()
             dist.all_reduce(h, group=group)
             out.copy_(h)
