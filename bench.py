@@ -447,14 +447,14 @@ def main():
                                "LDS-DMA + ds_read_b64_tr_b16, bf16 MFMA)"}
                  if d256 else
                  {"moe_fwd": f"chain_fwd_kernel (fused MoE expert chains, forward, {form} MFMA)",
-                  "moe_bwd": "chain_bwd_kernel (fused MoE expert chains, backward, "
-                             + ("fp32" if dtype == "fp32" else "bf16") + " MFMA)",
-                  "wgrad": f"pgemm_x6_kernel+pgemm_reduce_kernel (weight gradients, {form} MFMA)"})
+                  "moe_bwd": f"chain_bwd_kernel (fused MoE expert chains, backward, {form} MFMA)",
+                  # d <= 128: the wide kernel's design at a 128 x 128 output (engine.cpp wgrad128_on)
+                  "wgrad": (f"pgemm_x6w_kernel<TW=128>+pgemm_reduce_kernel (weight gradients, 128x128 {form} MFMA)"
+                            if m["n_attn_hidden_dim"] <= 128 else
+                            f"pgemm_x6_kernel+pgemm_reduce_kernel (weight gradients, {form} MFMA)")})
         rk = M["rkind"]
         if dtype == "bf16" and m["n_attn_hidden_dim"] <= 256:
             pipe, pipe_peak = "bf16 MFMA (one product per block)", BF16_MFMA_PEAK_TFLOPS
-        elif not d256 and rk == "moe_bwd":
-            pipe, pipe_peak = "fp32 MFMA", FP32_MFMA_PEAK_TFLOPS
         else:
             pipe, pipe_peak = "bf16 MFMA, six per fp32 block product (bf16x6)", BF16_MFMA_PEAK_TFLOPS / 6
         traffic = None
