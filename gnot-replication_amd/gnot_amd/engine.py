@@ -59,6 +59,14 @@ class Engine:
         ws = [lin.weight for lin in self.linears]
         bs = [lin.bias for lin in self.linears]
         for t in ws + bs:
+            if t.dtype in (torch.bfloat16, torch.float16):
+                # the reference's bf16 route (module cast / autocast) is the bf16 arithmetic mode here, on fp32
+                # parameters
+                raise RuntimeError(f"gnot_amd parameters must stay float32 (got {t.dtype}): keep the module in "
+                                   "fp32 and call set_precision('bf16') for bf16 arithmetic")
+            if t.dtype == torch.float64:
+                raise RuntimeError("gnot_amd computes in fp32 on the MFMA path; float64 modules are not supported "
+                                   "(the fp64 restatement is oracle/gnot_oracle.py, test infrastructure)")
             if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()):
                 raise RuntimeError("gnot_amd parameters must be contiguous float32 on a ROCm GPU")
         ptrs = tuple(t.data_ptr() for t in ws + bs)
