@@ -78,3 +78,18 @@ def test_set_precision_rejects_unknown_dtype():
     m = GNOT(3, 1, 3, 1, 1, 256, 2, 256, 256, 2, 8, 1)
     with pytest.raises(ValueError):
         m.set_precision("fp16")
+
+
+@pytest.mark.parametrize("cast", ["bfloat16", "float64"])
+def test_module_casts_raise_with_the_route(cast):
+    """The reference runs whatever dtype its module is cast to (model.py:142-173).  Here the parameters stay
+    fp32: a bf16 (or fp16) cast raises pointing at set_precision('bf16'), the bf16 arithmetic mode, and a
+    float64 cast raises naming the fp32 MFMA path."""
+    import torch
+    from gnot_amd import GNOT
+    m = GNOT(2, 1, 3, 1, 1, 32, 2, 32, 32, 2, 4, 1).cuda().to(getattr(torch, cast))
+    x = torch.rand(1, 50, 2, device="cuda")
+    th = torch.rand(1, 1, device="cuda")
+    fn = torch.rand(1, 20, 3, device="cuda")
+    with pytest.raises(RuntimeError, match="set_precision" if cast == "bfloat16" else "float64"):
+        m(x, th, [fn])
