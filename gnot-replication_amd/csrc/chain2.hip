@@ -535,9 +535,22 @@ __global__ void __launch_bounds__(64 * kC2Waves, 2) chain2_fwd_kernel(ChainArgs 
   float y[OTL][4];
   c2_split<DT, NP>(nx, bp);
   const int pin_last = B16 && SAVE ? store_in(save + (2 * nl - 1) * a.save_layer_stride, bp, KB) : 0;
-  c2f_layer<OTL, KB, false, SAVE, NP, B16>(pp, wp(nl - 1), bp, bsel, rs(nl - 1), svoff, nullptr, 0, nullptr, 0,
-                                           pend_next + pin_last, g, y);
+  // B16: the last Linear's output is not saved as such: slot nl-1 receives the bf16 score-scaled expert term
+  // below (the stage row itself; the backward divides d score by the score)
+  c2f_layer<OTL, KB, false, SAVE && !B16, NP, B16>(pp, wp(nl - 1), bp, bsel, rs(nl - 1), svoff, nullptr, 0, nullptr, 0,
+                                                   pend_next + pin_last, g, y);
   if constexpr (WALK) {
+    if constexpr (B16 && SAVE) {
+      // slot nl-1: the expert's bf16 score-scaled term (as the expert grid's stage row holds it)
+      const float s = valid ? a.scores[p * a.ldsc + e] : 0.f;
+      float t[OTL][4];
+#pragma unroll
+      for (int T = 0; T < OTL; ++T)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) t[T][r] = s * y[T][r];
+      round_rows_bf16<OTL>(t);
+      store_rows_b16<OTL>(t, rs(nl - 1), rowb, lane);
+    }
     // Y = base + sum_e s_e y_e, accumulated in place in expert order (Y == nullptr: MoE recompute, saves only)
     if (a.Y != nullptr) {
       const float s = valid ? a.scores[p * a.ldsc + e] : 0.f;
@@ -603,9 +616,18 @@ __global__ void __launch_bounds__(64 * kC2Waves, 2) chain2_fwd_kernel(ChainArgs 
   }
   if constexpr (OTL == 16) {
     if (a.combine != nullptr) {               // fused combine: write-through stage rows (D = 256)
+      // (B16 training: the engine points Y at save slot nl-1, so the stage row is the saved term)
       if constexpr (B16) store_rows_b16_sc1<OTL>(y, make_rsrc(a.Y + e * a.y_chain_stride + rbase, lay_b16), rowb, lane);
       else store_rows_sc1<OTL>(y, make_rsrc(a.Y + e * a.y_chain_stride + row0 * D, lay_bytes), voff);
       return;
+    }
+    if constexpr (B16 && SAVE) {
+      // bf16 training forward: the score-scaled term goes to save slot nl-1 (the backward's d score operand);
+      // with the combine pass the engine points Y at that same slot, so it is also the stage row
+      if (a.mode == CH_MOE) {
+        store_rows_b16<OTL>(y, rs(nl - 1), rowb, lane);
+        return;
+      }
     }
     if constexpr (B16) {
       if (a.stage_b16 && a.Y != nullptr) {    // bf16 stage rows for the moe_combine_b16 pass
@@ -853,6 +875,9 @@ __global__ void __launch_bounds__(64 * kC2Waves, 2) chain2_bwd_kernel(ChainArgs 
     ds += shfl_xor(ds, 16);
     ds += shfl_xor(ds, 32);
     const float s = valid ? a.scores[p * a.ldsc + e] : 0.f;
+    // B16: slot nl-1 holds bf16(s y) (the stage row, forward); d score = dq . y = (dq . s y) / s.  s = 0 (an
+    // underflowed softmax weight) contributes nothing to the gating gradient either way (it is scaled by s)
+    if constexpr (B16) ds = s != 0.f ? ds / s : 0.f;
     if (valid && g == 0) a.dscore[p * a.ldsc + e] += ds;
 #pragma unroll
     for (int T = 0; T < OTL; ++T)

@@ -1928,10 +1928,14 @@ static bool moe_fused(gnot_plan* p, bool bwd) {
 }
 // the bf16 mode's expert grid with the combine pass: bf16 stage rows and moe_combine_b16
 static bool moe_stage_b16(gnot_plan* p, bool bwd) { return p->b16s() && !p->moe_walk && !moe_fused(p, bwd); }
-static hipError_t launch_moe_pass(gnot_plan* p, const float* base, const float* stage, float* out, hipStream_t s) {
+// stage_stride: floats between two experts' stage rows (the stage buffer's P * D; the bf16 training forward's
+// stage rows are its save slot nl-1, one save chain apart)
+static hipError_t launch_moe_pass(gnot_plan* p, const float* base, const float* stage, float* out, hipStream_t s,
+                                  long stage_stride = 0) {
   const long P = p->P, D = p->D;
-  return p->b16s() ? launch_moe_combine_b16(base, stage, P * D, p->E, out, P, s)
-                   : launch_moe_combine(base, stage, P * D, p->E, out, P * D, s);
+  if (stage_stride == 0) stage_stride = P * D;
+  return p->b16s() ? launch_moe_combine_b16(base, stage, stage_stride, p->E, out, P, s)
+                   : launch_moe_combine(base, stage, stage_stride, p->E, out, P * D, s);
 }
 // save (and dZ) layout of a soft-MoE chain call: fp32 [NL][P][D] per expert, or in bf16 mode 2 NL bf16
 // layers per expert (ChainArgs::b16s)
@@ -1956,6 +1960,12 @@ static int moe_forward(Ctx& c, const ChainTable& T, const float* in, const float
     a.walk = 1; a.Y = qout; a.base = qin;
   } else {
     a.Y = p->P_("stage"); a.y_chain_stride = P * D;
+    if (p->b16s() && save) {
+      // bf16 training: the experts' bf16 score-scaled terms are kept in save slot nl-1 (the backward's d score
+      // operand), so the stage rows ARE that slot (chain2.hip): no separate stage write
+      a.Y = save + (NL - 1) * a.save_layer_stride;
+      a.y_chain_stride = a.save_chain_stride;
+    }
     if (moe_fused(p, false)) { a.base = qin; a.combine = qout; a.counters = reinterpret_cast<int*>(p->P_("moe_cnt")); }
     a.stage_b16 = moe_stage_b16(p, false) ? 1 : 0;
   }
@@ -1963,7 +1973,7 @@ static int moe_forward(Ctx& c, const ChainTable& T, const float* in, const float
     ProfScope ps(c, "moe_fwd", 2.0 * E * P * NL * (double)D * D);
     GNOT_CK(launch_chain_fwd(cw_scratch(p, a, c.s), c.s));
   }
-  if (!walk && !moe_fused(p, false)) GNOT_CK(launch_moe_pass(p, qin, p->P_("stage"), qout, c.s));
+  if (!walk && !moe_fused(p, false)) GNOT_CK(launch_moe_pass(p, qin, a.Y, qout, c.s, a.y_chain_stride));
   return GNOT_OK;
 }
 

@@ -133,8 +133,9 @@ struct ChainArgs {
   // CH_MOE, d = 256, np = 1 (bf16 mode): bf16 activation storage.  Saves and dZ are bf16 "pair-
   // interleaved" rows (gnot_common.h, 512 B per point; strides above then count 4-byte units, so a
   // [P, 256] bf16 layer is P * 128 of them).  Per chain, save slots 0 .. nlin-2 hold gelu'(h_l) of the
-  // GELU layers (the backward's factor, computed with gelu(h_l) in the forward), slot nlin-1 the expert
-  // output y (read back for d score), slots nlin + l the RNE bf16 input of Linear l (= gelu(h_{l-1}), the
+  // GELU layers (the backward's factor, computed with gelu(h_l) in the forward), slot nlin-1 the expert's
+  // bf16 score-scaled term s y (the stage row the combine sums; the backward's d score = dq . (s y) / s),
+  // slots nlin + l the RNE bf16 input of Linear l (= gelu(h_{l-1}), the
   // MFMA operand the forward used), written for the weight gradients; slot nlin + 0 (the shared MoE
   // input) only in chain 0.
   int b16s = 0;
