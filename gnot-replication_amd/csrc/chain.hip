@@ -155,11 +155,23 @@ chain_bwd_kernel(ChainArgs a) {
   // chunk of a KT-deep, OT-wide transposed image: fp32 fragment tiles, or NP-piece k-major blocks
   auto cf4 = [](int KT, int OT) { return BX ? x6_chunk_f4<D, NP>(KT, OT) : chunk_f4(KT, OT); };
   // acc += W^T in over the KT-deep image Wg (the weight stream of the pipe of this arithmetic)
+  float gr[DT][4];
+  float hs[DT][4];
+  // `late` (x6 / one-piece pipes): after the last weight chunk's barrier, before its MFMAs -- the saved
+  // pre-activations loaded by `hook` have landed by then, and gelu'(h) evaluates beside the MFMAs instead of
+  // as a VALU phase after them (bitwise the same values)
   auto mm = [&](auto KTc, auto OTc, const float4* Wg, const float4* nW, int nf4, const float (&in)[decltype(KTc)::value][4],
-                f32x4 (&acc)[decltype(OTc)::value], auto hook) __attribute__((always_inline)) {
+                f32x4 (&acc)[decltype(OTc)::value], auto hook, auto late) __attribute__((always_inline)) {
     constexpr int KT = decltype(KTc)::value, OT = decltype(OTc)::value;
-    if constexpr (BX) mm_tiles_pipe_x6<D, KT, OT, NP>(Wg, nW, nf4, wlds, cnt, in, acc, kChainWaves, wave, lane, hook);
-    else mm_tiles_pipe<KT, OT>(Wg, nW, nf4, wlds, cnt, in, acc, kChainWaves, wave, lane, hook);
+    if constexpr (BX) mm_tiles_pipe_x6<D, KT, OT, NP>(Wg, nW, nf4, wlds, cnt, in, acc, kChainWaves, wave, lane, hook, late);
+    else { mm_tiles_pipe<KT, OT>(Wg, nW, nf4, wlds, cnt, in, acc, kChainWaves, wave, lane, hook); late(); }
+  };
+  // hs := gelu'(hs) in place (the factor of the next backward layer)
+  auto ggrad = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int T = 0; T < DT; ++T)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) hs[T][r] = gelu_grad(hs[T][r]);
   };
   using IOTL = std::integral_constant<int, OTL>;
   using IDT = std::integral_constant<int, DT>;
@@ -214,13 +226,11 @@ chain_bwd_kernel(ChainArgs a) {
 
   // ---- last Linear; the saved pre-activation of Linear nl-2 is prefetched during its MFMAs
   if (dz) store_rows<OTL>(dy, dz + (nl - 1) * a.dz_layer_stride, D, p, valid, 16 * OTL, lane);
-  float gr[DT][4];
-  float hs[DT][4];
   {
     f32x4 acc[DT];
     init_bias<DT>(acc, nullptr, lane);
     auto pre = [&]() { load_rows<DT>(hs, save + (nl - 2) * a.save_layer_stride, D, p, valid, D, lane); };
-    mm(IOTL{}, IDT{}, L[nl - 1].WpT, next_W(nl - 1), next_f4(nl - 1), dy, acc, pre);
+    mm(IOTL{}, IDT{}, L[nl - 1].WpT, next_W(nl - 1), next_f4(nl - 1), dy, acc, pre, ggrad);
     acc_to_regs<DT>(acc, gr);
   }
   // ---- hidden Linears, reverse
@@ -228,24 +238,24 @@ chain_bwd_kernel(ChainArgs a) {
 #pragma unroll
     for (int T = 0; T < DT; ++T)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) gr[T][r] *= gelu_grad(hs[T][r]);
+      for (int r = 0; r < 4; ++r) gr[T][r] *= hs[T][r];     // hs = gelu'(h_l), evaluated during the MFMAs
     if (dz) store_rows<DT>(gr, dz + l * a.dz_layer_stride, D, p, valid, D, lane);
     f32x4 acc[DT];
     init_bias<DT>(acc, nullptr, lane);
     auto pre = [&]() { load_rows<DT>(hs, save + (l - 1) * a.save_layer_stride, D, p, valid, D, lane); };
-    mm(IDT{}, IDT{}, L[l].WpT, next_W(l), next_f4(l), gr, acc, pre);
+    mm(IDT{}, IDT{}, L[l].WpT, next_W(l), next_f4(l), gr, acc, pre, ggrad);
     acc_to_regs<DT>(acc, gr);
   }
-  // ---- first Linear (hs now holds the saved pre-activation of Linear 0)
+  // ---- first Linear (hs now holds gelu' of the saved pre-activation of Linear 0)
 #pragma unroll
   for (int T = 0; T < DT; ++T)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) gr[T][r] *= gelu_grad(hs[T][r]);
+    for (int r = 0; r < 4; ++r) gr[T][r] *= hs[T][r];
   if (dz) store_rows<DT>(gr, dz, D, p, valid, D, lane);
   if (a.dX) {
     f32x4 acc[KT0];
     init_bias<KT0>(acc, nullptr, lane);
-    mm(IDT{}, IKT0{}, L[0].WpT, nullptr, 0, gr, acc, NoHook());
+    mm(IDT{}, IKT0{}, L[0].WpT, nullptr, 0, gr, acc, NoHook(), NoHook());
     float dx[KT0][4];
     acc_to_regs<KT0>(acc, dx);
     store_rows<KT0>(dx, a.dX + e * a.dx_chain_stride, a.lddx, p, valid, a.in_dim, lane);

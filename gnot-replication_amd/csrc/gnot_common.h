@@ -481,10 +481,11 @@ GNOT_DEV f32x4 mfma_bf16(const u32x4& a, const u32x4& b, f32x4 c) {
 // the tile's one accumulator, smallest terms first (a single accumulation chain of
 // v_mfma_f32_16x16x32_bf16 issues at full rate, MI355X_MICROARCH.md).  NP = 1 (bf16 mode, one-piece
 // k-major images, pack x6 = 4): one product per block, the input rounded to bf16 (RNE).
-template <int D, int KT, int OT, int NP = 3, typename Hook = NoHook>
+// `late` runs after the LAST chunk's barrier, before its MFMAs (its VALU then issues beside them)
+template <int D, int KT, int OT, int NP = 3, typename Hook = NoHook, typename Late = NoHook>
 GNOT_DEV void mm_tiles_pipe_x6(const float4* __restrict__ Wg, const float4* __restrict__ next_W, int next_f4,
                                float4* lds, int& cnt, const float (&in)[KT][4], f32x4 (&acc)[OT], int nwaves,
-                               int wave, int lane, Hook hook = Hook()) {
+                               int wave, int lane, Hook hook = Hook(), Late late = Late()) {
   constexpr int kBufF4 = x6_buf_f4(D);
   constexpr int KB = (KT + 1) / 2;
   constexpr int OCH = x6_och<D, NP>(KT, OT);
@@ -506,6 +507,7 @@ GNOT_DEV void mm_tiles_pipe_x6(const float4* __restrict__ Wg, const float4* __re
       if (c + 1 < NTG * NOG) stage_image(nb, Wg + (c + 1) * CH4, CH4, nwaves, wave, lane);
       else if (next_W) stage_image(nb, next_W, next_f4, nwaves, wave, lane);
       if (c == 0) hook();
+      if (c == NTG * NOG - 1) late();
       const u32x4* cb = reinterpret_cast<const u32x4*>(lds + (cnt & 1) * kBufF4);
 #pragma unroll
       for (int tt = 0; tt < TCH; ++tt)
