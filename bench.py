@@ -23,8 +23,9 @@ cfg5 = configs[4] (64 variable meshes, LPT sample-DP).  --points / --meshes resi
 value = all query points processed by all ranks / max-over-ranks wall time of the K timed steps.
 roofline: the kernel class with the most device time in an untimed profiled step (normally the
 weight-gradient GEMMs or the MoE chain backward), timed live with hipEvents on the stream it runs on
-during the timed steps; achieved = its algorithmic FLOPs per launch / average launch duration vs the
-fp32 MFMA peak (157.3 TFLOP/s, MI355X_MICROARCH.md; the arithmetic is fp32).
+during the timed steps; achieved = its algorithmic FLOPs per launch / average launch duration; frac =
+achieved / the peak of the pipe the kernel issues on (bf16x6: 2.5 PFLOP/s / 6; bf16 mode: 2.5 PFLOP/s;
+HBM-bound classes: 8 TB/s, MI355X_MICROARCH.md).
 cpu_baseline: the stock-torch CPU port of the reference (oracle/torch_port.py) on this host's cores, on
 a bounded sample of the same model (one mesh of at most 16,384 points), rank 0 at N=1 only.
 """
@@ -267,9 +268,75 @@ def cpu_baseline(w, steps=5, warmup=2):
                        f"points/s is flat in the mesh size (linear attention)")
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n, script=None, argv=None):
+    """`python bench.py --gpus N` without a launcher: start N rank processes of this same command (one
+    per GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* in their environment) as CHILDREN -- no exec, and no GPU
+    call in this parent -- wait for all, and return the first non-zero exit code (the other ranks are
+    then ended by PID).  Only rank 0 prints the JSON line."""
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"), MASTER_PORT=port,
+                   GNOT_BENCH_SPAWNED="1")
+        procs.append(subprocess.Popen([sys.executable, script or os.path.abspath(__file__)]
+                                      + list(sys.argv[1:] if argv is None else argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                print(f"[bench] rank {procs.index(p)} exited with {code}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                for q in live:
+                    q.terminate()
+        time.sleep(0.2)
+    for p in procs:
+        p.wait()
+    return rc
+
+
+def resolve_world(args):
+    """(world, rank, local rank) of this process, or an exit: `--gpus N` with no WORLD_SIZE in the
+    environment spawns N ranks (spawn_ranks); with one (torchrun, or spawn_ranks' children) it must equal
+    --gpus.  N above the visible device count needs GNOT_BENCH_ONE_GPU=1 (every rank on cuda:0).
+    torch.cuda.device_count() does not initialise the GPU on this image."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        n = args.gpus or 1
+        if n > 1:
+            if n > torch.cuda.device_count() and not os.environ.get("GNOT_BENCH_ONE_GPU"):
+                raise SystemExit(f"bench.py: --gpus {n} but {torch.cuda.device_count()} GPU(s) visible "
+                                 "(GNOT_BENCH_ONE_GPU=1 runs every rank on cuda:0)")
+            raise SystemExit(spawn_ranks(n))
+        return 1, 0, 0
+    world = int(env_world)
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (launcher and flag disagree)")
+    if world > torch.cuda.device_count() and not os.environ.get("GNOT_BENCH_ONE_GPU"):
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but {torch.cuda.device_count()} GPU(s) visible "
+                         "(GNOT_BENCH_ONE_GPU=1 runs every rank on cuda:0)")
+    return world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU).  Without a launcher, N > 1 spawns the N rank processes itself; "
+                         "under torchrun it must equal WORLD_SIZE.  Default: WORLD_SIZE, else 1")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default=None, choices=sorted(WORKLOADS),
@@ -298,9 +365,7 @@ def main():
                          "main.py:41's shuffled DataLoader does; eager launches")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = resolve_world(args)
     # rehearsal knobs for the multi-process path on a one-GPU box (the real run is RCCL, one GPU per
     # rank): GNOT_BENCH_BACKEND=gloo (host-staged collectives) and GNOT_BENCH_ONE_GPU=1 (every rank on
     # cuda:0)
@@ -430,14 +495,14 @@ def main():
         opt_step()
 
     def roofline(M, dtype):
-        """the device-time-dominant kernel class of a measure() run.  `frac` is against the dense MFMA peak of
-        the path's arithmetic type (fp32 runs: the fp32 MFMA rate; bf16 mode: the bf16 rate).  `frac_pipe` is
-        against the pipe the kernel actually issues on: the bf16x6 kernels run six bf16 MFMAs per fp32 block
-        product, so their hardware ceiling is 2.5 PFLOP/s / 6 of fp32-equivalent work (bf16 mode: / 1)."""
+        """the device-time-dominant kernel class of a measure() run.  `frac` = achieved / the peak of the pipe
+        the kernel ISSUES on (never above 1): the fp32 path's bf16x6 kernels run six bf16 MFMAs per fp32
+        block product, so their ceiling is 2.5 PFLOP/s / 6 = 416.7 TFLOP/s of fp32-equivalent work; the bf16
+        mode's one-piece kernels 2.5 PFLOP/s; the HBM-bound bf16-row weight gradients 8 TB/s.
+        `vs_fp32_mfma_peak` = achieved / the v_mfma_f32 rate (157.3), the fp32 arithmetic's own MFMA peak."""
         avg_ms = M["kms"] / max(M["klaunch"], 1)
         flops_launch = M["kflops"] / max(M["klaunch"], 1)
         ach = flops_launch / (avg_ms * 1e-3) / 1e12 if M["klaunch"] and M["kms"] > 0 else 0.0
-        peak = FP32_MFMA_PEAK_TFLOPS if dtype == "fp32" else BF16_MFMA_PEAK_TFLOPS
         form = "bf16x6" if dtype == "fp32" else "bf16"
         d256 = m["n_attn_hidden_dim"] == 256
         names = ({"moe_fwd": f"chain2_fwd_kernel (fused MoE expert chains, forward, {form} MFMA)",
@@ -481,12 +546,11 @@ def main():
             "class_ms_per_step": {k: round(v[0], 3) for k, v in M["kinds"].items()},
             "bound": "mfma",
             "achieved": round(ach, 3),
-            "peak": peak,
+            "peak": round(pipe_peak, 2),
             "unit": "TFLOP/s",
-            "frac": round(ach / peak, 4),
+            "frac": round(ach / pipe_peak, 4),
             "pipe": pipe,
-            "pipe_peak": round(pipe_peak, 2),
-            "frac_pipe": round(ach / pipe_peak, 4),
+            "vs_fp32_mfma_peak": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
             "traffic": traffic,
             # the measured HBM bytes per launch (PMC) over the live launch time: how far the class is from
             # the memory side of its roofline (the one-piece bf16 chains are nearer to it than to the MFMA's)
@@ -497,7 +561,15 @@ def main():
             "launches": M["klaunch"],
         }
 
-    M_graph = {"on": False}
+    M_graph = {"on": False, "fail": None}
+
+    def rebuild_engine():
+        """a fresh engine (plan, streams, workspace) with this run's settings (GNOT.engine() copies the
+        module's comm / grad-comm / recompute / precision settings into it)"""
+        nonlocal eng
+        model._engine = None
+        eng = model.engine()
+        eng.param_grads = bool(args.torch_adamw)
 
     def measure():
         """warm-up, class profile, capture, K timed steps -> timing of the current precision"""
@@ -542,6 +614,8 @@ def main():
             eng.profile_enable(rkind)
             g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             print("[bench] capturing", file=sys.stderr, flush=True)
+            if comm is not None and os.environ.get("GNOT_BENCH_FAIL_CAPTURE") == "1":
+                comm.fail_next_captured = True        # test knob: one collective callback fails mid-capture
             try:
                 with torch.cuda.graph(g_fb):
                     fwd_bwd()
@@ -552,7 +626,30 @@ def main():
             except Exception as ex:           # e.g. a collective the communicator cannot capture: stay eager
                 print(f"[bench] capture failed ({ex!r}); eager steps", file=sys.stderr, flush=True)
                 captured = False
+                M_graph["fail"] = f"{type(ex).__name__}: {str(ex).splitlines()[0][:160] if str(ex) else ''}"
+                try:
+                    torch.cuda.synchronize()
+                except Exception as ex2:
+                    print(f"[bench] synchronize after the failed capture: {ex2!r}", file=sys.stderr, flush=True)
+            if world > 1:
+                # every rank replays, or every rank runs eager: a rank whose capture failed must not pair its
+                # eager collectives with its peers' graph replays
+                ok = torch.tensor([1.0 if captured else 0.0], device=device)
+                dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+                if captured and ok.item() < 1.0:
+                    captured = False
+                    M_graph["fail"] = "a peer rank's capture failed"
+            if not captured:
+                # the failed capture may have left the plan's side streams (and its events) in an invalidated
+                # capture state: discard the engine -- new plan, streams and workspace -- before eager steps
+                rebuild_engine()
+                g_fb = g_opt = None
                 torch.cuda.synchronize()
+                eng.profile_enable(rkind)
+                eager_step()                  # the new plan's event pool for the profiled class
+                eng.profile_read()
+                torch.cuda.synchronize()
+                eng.profile_enable(rkind)
             print("[bench] captured" if captured else "[bench] eager", file=sys.stderr, flush=True)
 
             def graph_step():
@@ -616,7 +713,8 @@ def main():
                    "geometry": "new mesh order every step (--vary-geometry)" if batches is not None else "fixed",
                    "moe_recompute": recompute,
                    "parallelism": (f"point-shard{world}" if shard else f"sample-dp{world}") if (world > 1 or shard) else "single",
-                   "step": "pack+fwd+RelL2+bwd+AdamW (native loss, " + ("torch fused AdamW" if args.torch_adamw else "native flat AdamW") + ")" + (" (hipGraph replay)" if M_graph["on"] else " (eager)")},
+                   "step": "pack+fwd+RelL2+bwd+AdamW (native loss, " + ("torch fused AdamW" if args.torch_adamw else "native flat AdamW") + ")" + (" (hipGraph replay)" if M_graph["on"] else " (eager)")
+                           + (f"; graph capture failed ({M_graph['fail']}): fresh engine, eager steps" if M_graph["fail"] else "")},
         "roofline": roofline(M0, args.dtype),
     }
     if (args.dtype == "fp32" and not args.fp32_only and world == 1 and m["n_attn_hidden_dim"] == 256

@@ -1662,12 +1662,15 @@ hipEvent_t next_event(gnot_plan* p) {
 // before the main stream overwrites `buf`, wait for the side-stream group that last read it
 int flush_deferred(Ctx& c);
 int guard_write(Ctx& c, const float* buf) {
-  for (const auto& d : c.p->deferred)         // a deferred group reads buf: launch it (and register) first
-    if (std::find(d.reads.begin(), d.reads.end(), buf) != d.reads.end()) {
-      const int rc = flush_deferred(c);
-      if (rc != GNOT_OK) return rc;
-      break;
-    }
+  // a deferred group reads buf: launch it (and register) first.  flush_deferred empties the vector, so
+  // decide before calling it
+  const auto& dq = c.p->deferred;
+  if (std::any_of(dq.begin(), dq.end(), [buf](const gnot_plan::DeferredWgrad& d) {
+        return std::find(d.reads.begin(), d.reads.end(), buf) != d.reads.end();
+      })) {
+    const int rc = flush_deferred(c);
+    if (rc != GNOT_OK) return rc;
+  }
   auto it = c.p->readers.find(buf);
   if (it != c.p->readers.end()) {
     GNOT_CK(hipStreamWaitEvent(c.s, it->second, 0));
@@ -2168,6 +2171,10 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
   // the input-function branch again runs on side2, concurrently with the query encoder and gating
   const bool br = p->I > 0;
   Ctx cf{p, br ? p->side2 : c.s};
+  // ranks issue their gradient collectives in one host order whatever serial_wgrad() says (it is chosen
+  // per rank from the local point count): a forked rank still holds the last attention call's groups
+  // (wg_cross[0]) deferred here, and side2 issues its groups' all-reduces at once -- flush first
+  if (p->grad_comm_on) GNOT_RUN(flush_deferred(c));
   if (br) {
     hipEvent_t fork = next_event(p);
     GNOT_CK(hipEventRecord(fork, c.s));

@@ -4,6 +4,8 @@ All device memory is a torch tensor (the PyTorch caching allocator owns it); the
 only receives pointers.  Kernel launches go on torch's current HIP stream.
 """
 import ctypes
+import itertools
+import weakref
 
 import torch
 
@@ -46,6 +48,18 @@ class Engine:
         self.bf16 = False          # bf16 arithmetic mode of the MFMA kernels up to d = 256 (gnot_plan_set_precision)
         self.input_grads = False   # also differentiate x, theta, input functions (gnot_plan_set_input_grads)
         self.fwd_token = 0
+        self.pending = None        # weakref to the autograd node of a training forward awaiting its backward
+        self.pending_seq = 0
+
+    _seq = itertools.count(1)
+
+    def busy(self):
+        """True while a training forward's backward is pending on this engine's activations."""
+        return self.pending is not None and self.pending() is not None
+
+    def mark_pending(self, node):
+        self.pending = weakref.ref(node) if node is not None else None
+        self.pending_seq = next(Engine._seq)
 
     def __del__(self):
         try:
@@ -167,7 +181,15 @@ class Engine:
         """torch's current stream ON THE WORKSPACE'S DEVICE (not the current device's)."""
         return ctypes.c_void_p(torch.cuda.current_stream(self.ws.device).cuda_stream)
 
+    def _own_comms(self):
+        """the communicators view raw pointers through ONE workspace tensor: this engine's, for its calls
+        (another engine of the same module may have been prepared since)"""
+        for c in (self.comm, self.grad_comm):
+            if c is not None:
+                c.ws = self.ws
+
     def forward(self, x, theta, fns, out):
+        self._own_comms()
         s = self.stream()
         _lib.check(self.lib.gnot_pack_weights(self.plan, s))
         fptr = _ptr_array([f.data_ptr() for f in fns]) if fns else None
@@ -180,10 +202,12 @@ class Engine:
         (None entries are skipped); launched on torch's current stream."""
         ptr = lambda t: t.data_ptr() if t is not None else None
         fptr = _ptr_array([ptr(f) for f in dfns]) if dfns else None
+        self._own_comms()
         with torch.cuda.device(self.ws.device):
             _lib.check(self.lib.gnot_input_grads(self.plan, ptr(dx), ptr(dtheta), fptr, self.stream()))
 
     def backward(self, dout):
+        self._own_comms()
         with torch.cuda.device(self.ws.device):
             _lib.check(self.lib.gnot_backward(self.plan, dout.data_ptr(), self.stream()))
         if self.grad_hook is not None:

@@ -15,6 +15,8 @@ Only the whole-model forward/backward runs on the GPU through libgnot_hip.so (on
 Function); the submodules exist to own the parameters.  There is no CPU path: on a tensor that is
 not on a ROCm device the forward raises.
 """
+import weakref
+
 import torch
 import torch.nn as nn
 
@@ -103,9 +105,11 @@ class _GNOTFunction(torch.autograd.Function):
     def backward(ctx, dout):
         eng = ctx.engine
         if eng.fwd_token != ctx.token:
-            raise RuntimeError("gnot_amd keeps the activations of the most recent forward only; "
-                               "backward must follow its own forward")
+            raise RuntimeError("gnot_amd: the activations of this forward were reused by a later forward (at most "
+                               "GNOT.max_pending_backwards training forwards may await their backward at once; "
+                               "raise it with GNOT.set_max_pending_backwards)")
         eng.backward(dout.contiguous().float())
+        eng.pending = None
         nfn = ctx.nfn
         need = ctx.needs_input_grad
         in_grads = [None] * (2 + nfn)
@@ -151,7 +155,9 @@ class GNOT(nn.Module):
                          n_mlp_num_layers=n_mlp_num_layers, n_mlp_hidden_dim=n_mlp_hidden_dim,
                          n_input_hidden_dim=n_input_hidden_dim, n_expert=n_expert, n_head=n_head,
                          n_input_functions=n_input_functions)
-        self._engine = None
+        self._engine = None        # the primary engine: every forward whose predecessor's backward has run
+        self._extra = []           # more engines, for forwards issued while earlier ones await their backward
+        self.max_pending_backwards = 2
         self._comm = None          # parallel.PointShardComm (set_point_shard); survives engine rebuilds
         self._grad_comm = None     # parallel.PointShardComm (set_grad_allreduce)
         self._moe_recompute = False
@@ -166,14 +172,49 @@ class GNOT(nn.Module):
             out += blk.linears()
         return out + self.out.linears()
 
+    def _new_engine(self):
+        e = Engine(self._cfg, self.linears())
+        e.comm = self._comm
+        e.grad_comm = self._grad_comm
+        e.moe_recompute = self._moe_recompute
+        e.bf16 = self._bf16
+        return e
+
     def engine(self):
+        """The primary engine (plan + workspace): the one every forward uses unless an earlier forward's
+        backward is still pending on it."""
         if self._engine is None:
-            self._engine = Engine(self._cfg, self.linears())
-            self._engine.comm = self._comm
-            self._engine.grad_comm = self._grad_comm
-            self._engine.moe_recompute = self._moe_recompute
-            self._engine.bf16 = self._bf16
+            self._engine = self._new_engine()
+            self._extra = []
         return self._engine
+
+    def set_max_pending_backwards(self, n):
+        """How many training forwards may await their backward at once (default 2).  The reference
+        builds a fresh autograd graph per call (model.py:154-173), so `f(a) + f(b)` or gradient
+        accumulation over several forwards work there; here every pending forward holds one engine's
+        activation set (its own workspace), so this bounds the memory.  A forward beyond the bound
+        reuses the oldest pending engine, whose backward then raises."""
+        if int(n) < 1:
+            raise ValueError("max_pending_backwards must be >= 1")
+        self.max_pending_backwards = int(n)
+
+    def _engine_for(self, training):
+        """An engine with no pending backward (forwards under no_grad, e.g. an evaluation between a
+        training forward and its backward, never disturb a pending one), created on demand; when
+        `max_pending_backwards` training forwards are pending, the oldest one's engine."""
+        prim = self.engine()
+        pool = [prim] + self._extra
+        for e in pool:
+            if not e.busy():
+                return e
+        busy = [e for e in pool if e.busy()]
+        if training and len(busy) >= self.max_pending_backwards:
+            return min(busy, key=lambda e: e.pending_seq)
+        e = self._new_engine()
+        e.param_grads = prim.param_grads
+        e.grad_hook = prim.grad_hook
+        self._extra.append(e)
+        return e
 
     def set_precision(self, dtype):
         """'fp32' (default: the reference's fp32 arithmetic, bf16x6-exact on the MFMA) or 'bf16' (BASELINE
@@ -191,6 +232,7 @@ class GNOT(nn.Module):
         else:
             raise ValueError(f"precision must be 'fp32' or 'bf16', got {dtype!r}")
         self.engine().bf16 = self._bf16
+        self._extra = []           # settings changed: spare engines are rebuilt on demand
 
     def set_moe_recompute(self, on=True):
         """Memory option (no reference counterpart; torch.utils.checkpoint is the analogue): keep only
@@ -199,10 +241,12 @@ class GNOT(nn.Module):
         Same results; one more MoE forward per call."""
         self._moe_recompute = bool(on)
         self.engine().moe_recompute = self._moe_recompute
+        self._extra = []
 
     def _apply(self, fn, *args, **kwargs):
         # moving / casting the module invalidates the bound parameter pointers
         self._engine = None
+        self._extra = []
         return super()._apply(fn, *args, **kwargs)
 
     def forward(self, x, theta, input_functions=None):
@@ -229,6 +273,7 @@ class GNOT(nn.Module):
         self._comm = comm
         self.engine().comm = comm
         self.engine().geom = None
+        self._extra = []
 
     def set_grad_allreduce(self, comm):
         """Sum the parameter gradients over the ranks of `comm` (gnot_amd.parallel.PointShardComm) INSIDE
@@ -238,6 +283,7 @@ class GNOT(nn.Module):
         self._grad_comm = comm
         self.engine().grad_comm = comm
         self.engine().geom = None
+        self._extra = []
 
     def forward_packed(self, x, x_off, theta, fns=(), fn_offs=(), n_global=None):
         """Packed-offsets forward (no padding): x [sum N_b, input_dim] with host offsets x_off [B+1];
@@ -254,10 +300,14 @@ class GNOT(nn.Module):
         grad = torch.is_grad_enabled()
         inputs_grad = grad and (x.requires_grad or theta.requires_grad or any(f.requires_grad for f in fns))
         training = grad and (inputs_grad or any(p.requires_grad for p in params))
-        eng = self.engine()
+        eng = self._engine_for(training)
         eng.input_grads = inputs_grad
         # every launch (and the plan's side streams) on x's device, whatever device is current
         with torch.cuda.device(x.device):
             eng.prepare([int(v) for v in x_off], [[int(v) for v in o] for o in fn_offs], training, x.device,
                         n_global=None if n_global is None else [int(n) for n in n_global])
-            return _GNOTFunction.apply(eng, self._cfg["out_dim"], len(fns), x, theta, *fns, *params)
+            out = _GNOTFunction.apply(eng, self._cfg["out_dim"], len(fns), x, theta, *fns, *params)
+        # the engine's activations now belong to this autograd node until its backward runs or the graph is
+        # freed (the node is only weakly referenced)
+        eng.mark_pending(out.grad_fn if training else None)
+        return out

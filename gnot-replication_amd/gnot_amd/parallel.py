@@ -88,6 +88,7 @@ class PointShardComm:
         self.world = dist.get_world_size(group)
         self.stage = stage_via_host
         self.ws = None                        # the engine's uint8 workspace tensor (set by Engine)
+        self.fail_next_captured = False       # test knob: the next collective issued under capture fails
         self._ar = _lib.ALLREDUCE_FN(self._allreduce)
         self._a2a = _lib.ALLTOALLV_FN(self._alltoallv)
         self.struct = _lib.GnotComm(None, self._ar, self._a2a)
@@ -108,11 +109,17 @@ class PointShardComm:
             return torch.cuda.stream(torch.cuda.default_stream(self.ws.device))
         return torch.cuda.stream(torch.cuda.ExternalStream(int(stream), device=self.ws.device))
 
+    def _injected_failure(self):
+        if self.fail_next_captured and torch.cuda.is_current_stream_capturing():
+            self.fail_next_captured = False
+            raise RuntimeError("injected collective failure under capture (PointShardComm.fail_next_captured)")
+
     def _allreduce(self, user, buf, count, stream):
         try:
             if count > 0:
                 t = self._view(buf, count)
                 with self._on(stream):
+                    self._injected_failure()
                     if self.stage:
                         _no_capture()
                         # host staging (gloo, tests): the whole device first, then blocking copies.  Under

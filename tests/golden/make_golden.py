@@ -2,7 +2,7 @@
 
 Test infrastructure only.  Run HERE (the survey container), never on the GPU box:
 
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [case ...]
 
 It imports `/root/reference/model.py` unchanged (it only depends on torch), builds
 `GNOT(...)` (model.py:142-173) in float64, runs forward + backward with a fixed upstream
@@ -66,6 +66,22 @@ CASES = [
          cfg=dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=2, n_attn_layers=1,
                   d=48, n_mlp_num_layers=2, n_expert=2, n_head=3, n_input_functions=0),
          N=[29, 18], M=[]),
+    # round 6: the BASELINE workloads' head shapes.  Multi-head dh = 32 (the headline's attention kernels
+    # are templated on dh; configs[2] runs dh = 32 with H = 8)
+    dict(name="d64_h2_mh", mode="packed", sharp=4.0, fp32_params=True,
+         cfg=dict(input_dim=3, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=2,
+                  d=64, n_mlp_num_layers=2, n_expert=3, n_head=2, n_input_functions=1),
+         N=[150, 97], M=[[60, 41]]),
+    # configs[2]'s expert count and MLP depth (E = 8, nl = 4) at a small width
+    dict(name="d32_e8_nl4", mode="padded", fp32_params=True,
+         cfg=dict(input_dim=3, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=2,
+                  d=32, n_mlp_num_layers=4, n_expert=8, n_head=4, n_input_functions=1),
+         N=[80, 64], M=[[30, 25]]),
+    # configs[1]'s shape: d = 128, 8 heads (dh = 16), 4 experts, 2 input functions (one block)
+    dict(name="d128_h8_e4_i2", mode="packed", sharp=3.0, fp32_params=True,
+         cfg=dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=1,
+                  d=128, n_mlp_num_layers=1, n_expert=4, n_head=8, n_input_functions=2),
+         N=[120, 75], M=[[50, 30], [44, 20]]),
 ]
 
 
@@ -115,6 +131,12 @@ def run_case(model_mod, case, seed):
     model = build_model(model_mod, c)
     if case.get("sharp"):
         sharpen(model, case["sharp"])
+    if case.get("fp32_params"):
+        # fp32-representable weights, stored as float32 (exact): halves the fixture, and the fp32 GPU path
+        # runs on exactly the weights the float64 reference used
+        with torch.no_grad():
+            for p in model.parameters():
+                p.copy_(p.float().double())
     g = torch.Generator().manual_seed(1000 + seed)
     I = c["n_input_functions"]
     Ns = case["N"]
@@ -158,7 +180,7 @@ def run_case(model_mod, case, seed):
     arrs["G"] = cat(Gs)
     arrs["out"] = cat(outs)
     for k, v in model.state_dict().items():
-        arrs["p." + k] = v.numpy()
+        arrs["p." + k] = v.float().numpy() if case.get("fp32_params") else v.numpy()
     for k, p in model.named_parameters():
         arrs["g." + k] = grads64[k].numpy()
         g32 = dict(m32.named_parameters())[k].grad.double()
@@ -175,7 +197,10 @@ def main():
     sys.path.insert(0, REF)
     sys.dont_write_bytecode = True
     import model as model_mod  # /root/reference/model.py
+    only = set(sys.argv[1:])               # optional: case names to (re)generate
     for case in CASES:
+        if only and case["name"] not in only:
+            continue
         arrs = run_case(model_mod, case, seed=7)
         path = os.path.join(HERE, case["name"] + ".npz")
         np.savez_compressed(path, **arrs)

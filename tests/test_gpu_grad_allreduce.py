@@ -14,7 +14,10 @@ experts with the moe_combine pass.  GNOT_WGRAD_OVERLAP=0 forces the serial form:
 is then issued on the comm stream right behind the caller's stream, and at d = 256 the expert grid sums
 its experts with the FUSED combine (inter-workgroup hand-off, chain2.hip moe_combine_last) while the
 collectives of earlier groups and the other rank's kernels run beside it -- the setting of every N > 1
-bench run of configs[2]/[3].  Both forms must give the flat all-reduce's bits.
+bench run of configs[2]/[3].  Both forms must give the flat all-reduce's bits -- also when the ranks take DIFFERENT forms ("mixed":
+serial_wgrad() is decided per rank from its local point count, so uneven sample-DP shares can split the
+ranks): every rank must still issue its gradient collectives in the same order (engine.cpp flushes the
+deferred groups before the input-function branch issues its own).
 The reference is single-device (main.py:27); SURVEY.md section 5 asks for the overlap.
 """
 import os
@@ -41,6 +44,8 @@ def _free_port():
 
 def _rank(rank, world, port, d, E, prec, overlap, q):
     sys.path[:0] = [ROOT, os.path.join(ROOT, "gnot-replication_amd"), os.path.join(ROOT, "tests")]
+    if overlap == "mixed":          # rank 0 forks its weight gradients, rank 1 runs them serially
+        overlap = "1" if rank == 0 else "0"
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GNOT_WGRAD_OVERLAP=overlap)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -78,7 +83,7 @@ def _rank(rank, world, port, d, E, prec, overlap, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("overlap", ["1", "0"])
+@pytest.mark.parametrize("overlap", ["1", "0", "mixed"])
 @pytest.mark.parametrize("d,E,prec", [(64, 3, "fp32"), (256, 8, "fp32"), (256, 8, "bf16")])
 def test_overlapped_grad_allreduce_equals_flat_allreduce(d, E, prec, overlap):
     world = 2

@@ -156,19 +156,69 @@ def test_repeated_steps_are_deterministic():
         assert np.array_equal(g1[k], g2[k]), k
 
 
-def test_backward_requires_matching_forward():
+def _inputs(fx):
+    dev = torch.device("cuda")
+    return (torch.from_numpy(fx["x"]).float().to(dev), fx["x_off"].tolist(),
+            torch.from_numpy(fx["theta"]).float().to(dev),
+            [torch.from_numpy(f).float().to(dev) for f in fx["fns"]], [o.tolist() for o in fx["fn_offs"]])
+
+
+def test_two_forwards_one_backward():
+    """The reference builds one autograd graph per call (model.py:154-173): f(a) + f(b) -> backward
+    sums both calls' gradients.  Two pending forwards use two engines (activation sets)."""
+    fx = load("cross2_packed")
+    m = build_model(fx["params"], fx["cfg"])
+    _, g1 = run_packed(m, fx, fx["G"])
+    x, xo, th, fns, fo = _inputs(fx)
+    G = torch.from_numpy(fx["G"]).float().cuda()
+    m.zero_grad(set_to_none=True)
+    o1 = m.forward_packed(x, xo, th, fns, fo)
+    o2 = m.forward_packed(x, xo, th, fns, fo)
+    ((o1 * G).sum() + (o2 * G).sum()).backward()
+    for k, p in m.named_parameters():
+        assert np.array_equal(p.grad.double().cpu().numpy(), 2 * g1[k]), k
+
+
+def test_eval_forward_between_forward_and_backward():
+    """forward(train) -> forward(no_grad, another geometry) -> backward: the pending backward keeps its
+    own activations (the evaluation runs on an engine with no pending backward)."""
+    fx = load("cross2_packed")
+    m = build_model(fx["params"], fx["cfg"])
+    out0, g0 = run_packed(m, fx, fx["G"])
+    x, xo, th, fns, fo = _inputs(fx)
+    m.zero_grad(set_to_none=True)
+    o = m.forward_packed(x, xo, th, fns, fo)
+    with torch.no_grad():                       # a different geometry: the first half of the points
+        n = max(1, xo[1] // 2)
+        e = m.forward_packed(x[:n].contiguous(), [0, n], th[:1].contiguous(),
+                             [f[: fo[i][1]].contiguous() for i, f in enumerate(fns)],
+                             [[0, fo[i][1]] for i in range(len(fns))])
+    assert torch.isfinite(e).all()
+    (o * torch.from_numpy(fx["G"]).float().cuda()).sum().backward()
+    assert np.array_equal(o.detach().double().cpu().numpy(), out0)
+    for k, p in m.named_parameters():
+        assert np.array_equal(p.grad.double().cpu().numpy(), g0[k]), k
+
+
+def test_pending_backward_bound():
+    """More pending training forwards than GNOT.max_pending_backwards: the oldest one's activations are
+    reused and its backward raises; a forward whose graph was freed releases its engine."""
     fx = load("tiny_n_lt_h")
     m = build_model(fx["params"], fx["cfg"])
-    dev = torch.device("cuda")
-    x = torch.from_numpy(fx["x"]).float().to(dev)
-    theta = torch.from_numpy(fx["theta"]).float().to(dev)
-    fns = [torch.from_numpy(f).float().to(dev) for f in fx["fns"]]
-    offs = [o.tolist() for o in fx["fn_offs"]]
-    o1 = m.forward_packed(x, fx["x_off"].tolist(), theta, fns, offs)
-    o2 = m.forward_packed(x, fx["x_off"].tolist(), theta, fns, offs)
-    with pytest.raises(RuntimeError, match="most recent forward"):
+    m.set_max_pending_backwards(1)
+    x, xo, th, fns, fo = _inputs(fx)
+    o1 = m.forward_packed(x, xo, th, fns, fo)
+    o2 = m.forward_packed(x, xo, th, fns, fo)
+    with pytest.raises(RuntimeError, match="reused by a later forward"):
         o1.sum().backward()
     o2.sum().backward()
+    m.set_max_pending_backwards(2)
+    o3 = m.forward_packed(x, xo, th, fns, fo)
+    del o3                                      # graph freed without a backward: its engine is free again
+    o4 = m.forward_packed(x, xo, th, fns, fo)
+    o5 = m.forward_packed(x, xo, th, fns, fo)
+    (o4.sum() + o5.sum()).backward()
+    assert len(m._extra) <= 1
 
 
 def test_eval_no_grad_matches_training_forward():
