@@ -432,7 +432,10 @@ def main():
                                            (ctypes.c_int64 * max(1, len(flat)))(*flat) if flat else None, 1))
         need = lib.gnot_plan_workspace_bytes(eng.plan)
         free, _ = torch.cuda.mem_get_info(device)
-        recompute = need > 0.85 * free        # headroom: RCCL buffers, allocator slack
+        # headroom for RCCL's buffers, the point-shard exchange tensors and allocator slack: 12 GiB (at N = 2 a
+        # configs[3] rank holds 524,288 points: 238 GiB of workspace, which fits a 288 GB MI355X without the
+        # recompute that would cost ~25 % of its step)
+        recompute = need > free - 12 * 2 ** 30
         eng.geom = None
     model.set_moe_recompute(recompute)
     model.set_precision(args.dtype)

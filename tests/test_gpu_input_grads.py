@@ -52,7 +52,7 @@ def _setup(name, seed=5):
 def _port_grads(cfg, sd64, xs, thetas, fns_per_sample, Gs, autocast=False):
     """float64 autograd of the port, one reference call per sample (packed offsets = B=1 calls).
     autocast=True: the same in fp32 under torch.autocast(bfloat16) on the CPU -- the reference's own
-    bf16 arithmetic (model.py run under autocast), the yardstick for the bf16 mode's input gradients."""
+    bf16 arithmetic (model.py run under autocast); diagnostics only."""
     from oracle import torch_port
     dt = torch.float32 if autocast else torch.float64
     sd = {k: v.to(dt) for k, v in sd64.items()}
@@ -125,21 +125,18 @@ def test_input_grads_packed_match_port(name, prec, walk, recompute, monkeypatch)
     e_all = _rel(np.concatenate([g.ravel() for g in got]), np.concatenate([r.ravel() for r in ref]))
     print(f"\ninput grads {name} {prec} walk={walk} recompute={recompute}: dx {errs[0]:.2e} dtheta {errs[1]:.2e} "
           f"dfns {errs[2:]} all {e_all:.2e}")
-    # fp32: every input gradient at 1e-4.  bf16 mode: norm-wise over all input gradients concatenated at 1e-2
-    # (the rule tests/test_gpu_bf16.py applies to the parameter gradients), and PER TENSOR at 1e-2 or twice
-    # the error of the reference's own bf16 arithmetic (the port under torch.autocast(bfloat16)) on that
-    # tensor, whichever is larger: d theta sums ~300 points' terms that largely cancel, and autocast itself
-    # misses it by ~1.1e-2 (d input functions ~1.7e-2) -- INTEGRATION.md section 4
+    # fp32: every input gradient at 1e-4.  bf16 mode: norm-wise over all input gradients concatenated at
+    # north_star's 1e-2 (the rule tests/test_gpu_bf16.py applies to the parameter gradients), and per tensor
+    # at a FIXED ceiling of 2e-2: d theta sums ~300 points' terms that largely cancel and d input function
+    # sums over the query points through the cross attention, so their relative error is amplified --
+    # measured 1.0e-2 / 1.2e-2 (profiles/r05b_input_grads_tests.log), the reference's own bf16 arithmetic
+    # (the port under torch.autocast(bfloat16)) misses them by 1.2e-2 / 1.5e-2
     assert e_all < tol, e_all
     if prec == "fp32":
         assert all(e < tol for e in errs), errs
     else:
-        ax, at, af = _port_grads(cfg, sd64, xs, thetas, fns_ps, Gs, autocast=True)
-        auto = [np.concatenate(ax), np.stack(at)] + [np.concatenate([af[b][i] for b in range(len(Ns))]) for i in range(I)]
-        e_auto = [_rel(a, r) for a, r in zip(auto, ref)]
-        print(f"torch bf16 autocast (reference arithmetic) per tensor: {['%.2e' % e for e in e_auto]}")
-        bad = [(k, e, ea) for k, (e, ea) in enumerate(zip(errs, e_auto)) if e > max(tol, 2 * ea)]
-        assert not bad, bad
+        assert errs[0] < tol, errs                         # dx: the bulk of the input gradients
+        assert all(e < 2e-2 for e in errs), errs
 
 
 def test_input_grads_require_a_backward_after_the_forward():
