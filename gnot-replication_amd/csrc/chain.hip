@@ -124,17 +124,15 @@ chain_fwd_kernel(ChainArgs a) {
   }
 }
 
-// NP = 3: exact fp32 MFMA on fp32 fragment images of W^T; NP = 1 (bf16 mode): one RNE bf16 piece per
-// operand on k-major one-piece images of W^T (pack x6 = 4), fp32 accumulation
+// NP = 3: bf16x6 on k-major 3-piece images of W^T (pack x6 = 1), as the forward (round 5; the exact fp32
+// MFMA on fp32 fragment images before); NP = 1 (bf16 mode): one RNE bf16 piece per operand on k-major
+// one-piece images of W^T (pack x6 = 4), fp32 accumulation
 // three waves per SIMD at d <= 128 (as the forward): 162-165 VGPRs without spills at d = 128, where the
 // compiler's own choice (132 VGPRs + 48 AGPRs) allowed two, so a configs[1] launch (2,500 waves) ran in two
-// rounds.  d = 112 would spill at three.  -DGNOT_CHAIN_BWD_OCC=1 builds the compiler's choice (A/B)
-#ifndef GNOT_CHAIN_BWD_OCC
-#define GNOT_CHAIN_BWD_OCC 3
-#endif
+// rounds.  d = 112 would spill at three
 template <int D, int KT0, int OTL, int NP>
 __global__ void __launch_bounds__(64 * kChainWaves)
-__attribute__((amdgpu_waves_per_eu((D <= 128 && D != 112) ? GNOT_CHAIN_BWD_OCC : 1)))
+__attribute__((amdgpu_waves_per_eu((D <= 128 && D != 112) ? 3 : 1)))
 chain_bwd_kernel(ChainArgs a) {
   constexpr int DT = D / 16;
   const int lane = threadIdx.x & 63;
@@ -147,13 +145,11 @@ chain_bwd_kernel(ChainArgs a) {
   const ChainLayer* L = a.layers + e * nl;
   const float* save = a.save + e * a.save_chain_stride;
   float* dz = a.dz ? a.dz + e * a.dz_chain_stride : nullptr;
-  // k-major NP-piece images of W^T on the bf16 MFMA (bf16 mode, and bf16x6 in the fp32 mode unless built
-  // with GNOT_CHAIN_BWD_FP32), or fp32 fragment images on the exact fp32 MFMA
-  constexpr bool BX = NP == 1 || kChainBwdX6;
-  __shared__ __attribute__((aligned(16))) float4 wlds[BX ? 2 * x6_buf_f4(D) : 2 * kChunkF4];
+  // k-major NP-piece images of W^T on the bf16 MFMA
+  __shared__ __attribute__((aligned(16))) float4 wlds[2 * x6_buf_f4(D)];
   int cnt = 0;
-  // chunk of a KT-deep, OT-wide transposed image: fp32 fragment tiles, or NP-piece k-major blocks
-  auto cf4 = [](int KT, int OT) { return BX ? x6_chunk_f4<D, NP>(KT, OT) : chunk_f4(KT, OT); };
+  // chunk of a KT-deep, OT-wide transposed image (NP-piece k-major blocks)
+  auto cf4 = [](int KT, int OT) { return x6_chunk_f4<D, NP>(KT, OT); };
   // acc += W^T in over the KT-deep image Wg (the weight stream of the pipe of this arithmetic)
   float gr[DT][4];
   float hs[DT][4];
@@ -163,8 +159,7 @@ chain_bwd_kernel(ChainArgs a) {
   auto mm = [&](auto KTc, auto OTc, const float4* Wg, const float4* nW, int nf4, const float (&in)[decltype(KTc)::value][4],
                 f32x4 (&acc)[decltype(OTc)::value], auto hook, auto late) __attribute__((always_inline)) {
     constexpr int KT = decltype(KTc)::value, OT = decltype(OTc)::value;
-    if constexpr (BX) mm_tiles_pipe_x6<D, KT, OT, NP>(Wg, nW, nf4, wlds, cnt, in, acc, kChainWaves, wave, lane, hook, late);
-    else { mm_tiles_pipe<KT, OT>(Wg, nW, nf4, wlds, cnt, in, acc, kChainWaves, wave, lane, hook); late(); }
+    mm_tiles_pipe_x6<D, KT, OT, NP>(Wg, nW, nf4, wlds, cnt, in, acc, kChainWaves, wave, lane, hook, late);
   };
   // hs := gelu'(hs) in place (the factor of the next backward layer)
   auto ggrad = [&]() __attribute__((always_inline)) {

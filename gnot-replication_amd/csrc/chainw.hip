@@ -113,7 +113,7 @@ hipError_t cw_linear(const float* X, long ldx, int K, int KT, const void* W, con
 
 hipError_t launch_chainw(const ChainArgs& a, bool bwd, hipStream_t s) {
   const int D = a.D, DT = D / 16, nl = a.nlin, P = a.P;
-  if (!a.layers_host || !a.scratch || nl < 2 || a.walk || a.combine) return hipErrorInvalidValue;
+  if (!a.layers_host || !a.scratch || nl < 2) return hipErrorInvalidValue;
   const long n = (long)P * D;
   float* s0 = a.scratch;                 // h (forward without saves) / g (backward)
   float* s1 = a.scratch + n;             // x = gelu(h)

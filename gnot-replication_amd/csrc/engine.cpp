@@ -223,12 +223,6 @@ struct gnot_plan {
   // input; the backward re-runs that call's expert forward into ONE shared save buffer ("mrsave")
   // just before its chain backward -- E*NL*P*D floats once instead of per MoE call
   bool moe_recompute = false;
-  // soft-MoE calls in the walk form (chain2.hip: one workgroup sums all experts in place, no [P, E, d]
-  // stage): decided per batch in gnot_plan_set_batch (chain2_walk_choice)
-  bool moe_walk = false;
-  // fused soft-MoE combine policy (moe_fused): 0 never (default), 1 every backward + the bf16-mode forward,
-  // 2 also the bf16x6 forward; GNOT_MOE_FUSED=0/1/2 overrides (read per batch)
-  int moe_fused_mode = 0;
   // input gradients (gnot_plan_set_input_grads): the x / gating / input-function encoders' first Linears
   // also run their backward-data into dxin / dxg / dfnin<i>
   bool input_grads = false;
@@ -542,8 +536,8 @@ static void plan_images(gnot_plan* p) {
       Img f = cw ? new_img(OTp, KTp) : new_img_x6(OTp, KTp, c2 ? c2np : b1 ? 1 : 3);
       const size_t bo = new_bias(16 * OTp);
       job(li, f, 0, 0, OTp, KTp, 0, (long)bo, cw ? 0 : c2 ? c2x6 : b1 ? 4 : 1);
-      // backward-data image: d <= 192 k-major x6 (kChainBwdX6) or one-piece (bf16 mode), else fp32 tiles
-      const bool tx6 = !c2 && !cw && (b1 || kChainBwdX6);
+      // backward-data image: d <= 192 k-major x6 or one-piece (bf16 mode), else fp32 tiles
+      const bool tx6 = !c2 && !cw;
       Img t = c2 ? new_img_x6(KTp, OTp, c2np) : tx6 ? new_img_x6(KTp, OTp, b1 ? 1 : 3) : new_img(KTp, OTp);
       job(li, t, 0, 0, KTp, OTp, 1, -1, c2 ? c2x6 : tx6 ? (b1 ? 4 : 1) : 0);
       p->fwd_img[li] = f;
@@ -626,15 +620,8 @@ static void plan_images(gnot_plan* p) {
 }
 
 // ====================================================================== point-reduction GEMM groups
-static bool wgrad128_on() {
-  const char* e = std::getenv("GNOT_WGRAD128");
-  return !(e && e[0] == '0');
-}
-// split-K target of the 128-wide kernel (GNOT_WGRAD128_WGS overrides: A/B runs)
-static long wide128_wgs() {
-  const char* e = std::getenv("GNOT_WGRAD128_WGS");
-  return e ? std::max(1L, std::atol(e)) : 128;
-}
+// split-K target of the 128-wide kernel
+constexpr long kWide128Wgs = 128;
 static void finish_group(gnot_plan* p, WgradGroup& G) {
   G.x6 = true;
   for (const auto& J : G.jobs)
@@ -651,15 +638,15 @@ static void finish_group(gnot_plan* p, WgradGroup& G) {
     if (J.out > 256 || J.in > 256) G.wide = false;
   G.tw = 256;
   // d <= 128 (configs[1]): the wide kernel's design at a 128 x 128 output (4 waves, staging interleaved with
-  // the MFMAs, raw rows by LDS-DMA) instead of the 128-tile kernel (GNOT_WGRAD128=0 keeps that one)
-  if (G.x6 && !G.wide && p->D <= 128 && !G.jobs.empty() && wgrad128_on()) {
+  // the MFMAs, raw rows by LDS-DMA) instead of the 128-tile kernel (round 5: configs[1] 3.44 -> 3.37 ms)
+  if (G.x6 && !G.wide && p->D <= 128 && !G.jobs.empty()) {
     bool fits = true;
     for (const auto& J : G.jobs)
       if (J.out > 128 || J.in > 128) fits = false;
     if (fits) { G.wide = true; G.tw = 128; }
   }
   if (G.b16) G.wide = true;          // the bf16-storage kernel has the wide kernel's geometry
-  const long target = G.wide ? (G.tw == 128 ? wide128_wgs() : wide_wgs) : G.x6 ? x6_wgs : kTargetWGs;
+  const long target = G.wide ? (G.tw == 128 ? kWide128Wgs : wide_wgs) : G.x6 ? x6_wgs : kTargetWGs;
   long tiles = 0;
   for (auto& J : G.jobs) {
     J.tiles_o = (J.out + kPTile - 1) / kPTile;
@@ -1261,18 +1248,11 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
     if (tr && !p->moe_recompute) C.add(s + "m2save", E * NL * P * D, D);
     C.add(s + "query2", P * D, D);
   }
-  p->moe_walk = p->D == 256 && p->L > 0 && chain2_walk_choice(P, E);
-  {
-    const char* f = std::getenv("GNOT_MOE_FUSED");
-    p->moe_fused_mode = (f && f[0] >= '0' && f[0] <= '2') ? f[0] - '0' : 0;
-  }
-  if (!p->moe_walk) C.add("stage", E * P * D, D);
+  C.add("stage", E * P * D, D);
   if (D > 256) {                             // chainw.hip scratch: query-branch chains / input-function branch
     C.add("lw_scr", 2 * P * D, D);
     if (I > 0) C.add("lw_scr2", 2 * Qmax * D, D);
   }
-  if (p->D == 256 && p->L > 0 && !p->moe_walk)        // fused-combine completion counters, one per 128 points
-    C.add("moe_cnt", (P + kC2Rows - 1) / kC2Rows, 0);
   if (tr && p->moe_recompute && p->L > 0) C.add("mrsave", E * NL * P * D, D);
   if (p->sharded) {                          // scramble exchange scratch: head-major rows / packed peers
     C.add("xa", P * D, p->Dr);
@@ -1528,9 +1508,6 @@ extern "C" int gnot_plan_bind_workspace_async(gnot_plan* p, void* workspace, siz
   // part of the workspace once per bind (the tables follow it, uploaded after this on the same stream)
   if (p->padded())
     GNOT_CK(hipMemsetAsync(p->ws, 0, p->bufs["__tables"].off, static_cast<hipStream_t>(stream)));
-  // the fused soft-MoE combine's completion counters start at zero (each launch leaves them at zero)
-  if (p->bufs.count("moe_cnt"))
-    GNOT_CK(hipMemsetAsync(p->P_("moe_cnt"), 0, ((p->P + kC2Rows - 1) / kC2Rows) * sizeof(int), static_cast<hipStream_t>(stream)));
   if (!p->side2) GNOT_CK(hipStreamCreateWithFlags(&p->side2, hipStreamNonBlocking));
   if (!p->side) {
     // same priority as the caller's stream: measured on MI355X, a low- (or high-) priority side
@@ -1911,26 +1888,10 @@ int attn_backward(Ctx& c, int l, bool cross) {
 
 }  // namespace
 
-// the soft-MoE experts of one call: walk form (d = 256, chain2.hip) or the expert grid, whose last
-// workgroup per 128-point block sums the experts (the fused combine, d = 256) or a moe_combine pass over
-// the [E, P, d] stage.  The fused combine runs in every backward at d = 256 and in the forward of the
-// bf16 mode (bf16 stage rows); the bf16x6 forward keeps the separate pass.  Measured at configs[2]
-// (262,144 points, E = 8; profiles/r04_chain_grid.txt): bf16x6 forward 6.76 ms + 0.47 pass against 7.51
-// fused, backward 8.27 + 0.47 against 8.73; bf16 storage forward 4.01 + 0.47 against 4.08 fused
-static bool moe_walk(gnot_plan* p) { return p->moe_walk; }
-// The expert grid's fused combine (the last workgroup of a 128-point block sums its E stage rows, chain2.hip
-// moe_combine_last: sc1 stores, counter, agent acquire -- valid beside any co-resident work) or the
-// moe_combine pass (bf16 mode: moe_combine_b16 over bf16 stage rows).  Every form gives the same bits
-// (tests/test_gpu_moe_walk.py, test_gpu_recompute.py).  Default: the pass.  One box, interleaved x2
-// (profiles/r05rf*): configs[2] fp32 229.9 / 230.4 ms (pass) vs 230.7 / 230.0 (fused backward) vs 232.9 /
-// 232.3 (fused everywhere); bf16 mode 92.6 / 93.3 vs 95.9 / 95.9 (the bf16 pass reads bf16 stage rows);
-// configs[0] 9.24 vs 9.30 ms, bf16 5.93 vs 6.13
-static bool moe_fused(gnot_plan* p, bool bwd) {
-  if (p->D != 256 || p->moe_walk || p->moe_fused_mode == 0) return false;
-  return p->moe_fused_mode == 2 || bwd || p->b16s();
-}
-// the bf16 mode's expert grid with the combine pass: bf16 stage rows and moe_combine_b16
-static bool moe_stage_b16(gnot_plan* p, bool bwd) { return p->b16s() && !p->moe_walk && !moe_fused(p, bwd); }
+// the soft-MoE experts of one call: the expert grid writes the [E, P, d] stage (bf16 mode at d = 256: bf16
+// stage rows), a moe_combine pass sums residual + experts in expert order (chain2.hip names the forms that
+// were measured slower and removed)
+static bool moe_stage_b16(gnot_plan* p) { return p->b16s(); }
 // stage_stride: floats between two experts' stage rows (the stage buffer's P * D; the bf16 training forward's
 // stage rows are its save slot nl-1, one save chain apart)
 static hipError_t launch_moe_pass(gnot_plan* p, const float* base, const float* stage, float* out, hipStream_t s,
@@ -1953,30 +1914,24 @@ static int moe_forward(Ctx& c, const ChainTable& T, const float* in, const float
   gnot_plan* p = c.p;
   const long P = p->P;
   const int D = p->D, E = p->E, NL = p->NL;
-  const bool walk = moe_walk(p);
   ChainArgs a = chain_args(p, T, P);
   a.X = in; a.ldx = D; a.ldy = D;
   a.scores = p->P_("scores"); a.ldsc = (int)p->bufs["scores"].ld; a.mode = CH_MOE;
   moe_save_strides(p, a);                 // bf16 mode: bf16 expert terms with or without saves
   a.save = save;
-  if (walk) {
-    a.walk = 1; a.Y = qout; a.base = qin;
-  } else {
-    a.Y = p->P_("stage"); a.y_chain_stride = P * D;
-    if (p->b16s() && save) {
-      // bf16 training: the experts' bf16 score-scaled terms are kept in save slot nl-1 (the backward's d score
-      // operand), so the stage rows ARE that slot (chain2.hip): no separate stage write
-      a.Y = save + (NL - 1) * a.save_layer_stride;
-      a.y_chain_stride = a.save_chain_stride;
-    }
-    if (moe_fused(p, false)) { a.base = qin; a.combine = qout; a.counters = reinterpret_cast<int*>(p->P_("moe_cnt")); }
-    a.stage_b16 = moe_stage_b16(p, false) ? 1 : 0;
+  a.Y = p->P_("stage"); a.y_chain_stride = P * D;
+  if (p->b16s() && save) {
+    // bf16 training: the experts' bf16 score-scaled terms are kept in save slot nl-1 (the backward's d score
+    // operand), so the stage rows ARE that slot (chain2.hip): no separate stage write
+    a.Y = save + (NL - 1) * a.save_layer_stride;
+    a.y_chain_stride = a.save_chain_stride;
   }
+  a.stage_b16 = moe_stage_b16(p) ? 1 : 0;
   {
     ProfScope ps(c, "moe_fwd", 2.0 * E * P * NL * (double)D * D);
     GNOT_CK(launch_chain_fwd(cw_scratch(p, a, c.s), c.s));
   }
-  if (!walk && !moe_fused(p, false)) GNOT_CK(launch_moe_pass(p, qin, a.Y, qout, c.s, a.y_chain_stride));
+  GNOT_CK(launch_moe_pass(p, qin, a.Y, qout, c.s, a.y_chain_stride));
   return GNOT_OK;
 }
 
@@ -2081,7 +2036,7 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
   const long P = p->P;
   const int D = p->D, E = p->E, NL = p->NL;
   float* dquery = p->P_("dquery");
-  float* stage = p->moe_walk ? nullptr : p->P_("stage");
+  float* stage = p->P_("stage");
   p->readers.clear();
   p->deferred.clear();
   if (p->grad_comm_on) {                   // the comm stream joins here (a first-level fork of the caller's)
@@ -2126,7 +2081,6 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
     a.dX = dquery; a.lddx = D; a.dx_chain_stride = 0;
     GNOT_RUN(chain_bwd(a, p->k_out(), P, p->wg_out, "chain_bwd"));
   }
-  const bool walk = moe_walk(p);
   for (int l = p->L - 1; l >= 0; --l) {
     const std::string s = "b" + std::to_string(l) + ".";
     // ffn2 experts: query2 = query1 + sum_e s_e ffn2_e(bb)   (model.py:134-137)
@@ -2141,7 +2095,6 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
         f.scores = p->P_("scores"); f.ldsc = (int)p->bufs["scores"].ld; f.mode = CH_MOE;
         f.save = mr; moe_save_strides(p, f);
         // only the saves are needed: no output (Y = null), no combine
-        f.walk = walk ? 1 : 0;
         f.Y = nullptr; f.y_chain_stride = P * D;
         ProfScope ps(c, "moe_recompute", 2.0 * E * P * NL * (double)D * D);
         GNOT_CK(launch_chain_fwd(cw_scratch(p, f, c.s), c.s));
@@ -2151,18 +2104,12 @@ extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
       a.scores = p->P_("scores"); a.ldsc = (int)p->bufs["scores"].ld; a.dscore = p->P_("dscore");
       a.save = p->P_(p->msave(l, m1)); moe_save_strides(p, a);
       float* dsum = p->P_(p->dsum_buf(m1));
-      // d(MoE input) = sum_e W_e0^T dz_e0: summed in place by the walk form, by the expert grid's fused
-      // combine (d = 256), or by moe_combine over the stage
+      // d(MoE input) = sum_e W_e0^T dz_e0: each expert's term into the stage, summed by moe_combine
       GNOT_RUN(guard_write(c, dsum));
-      if (walk) {
-        a.walk = 1; a.dX = dsum; a.lddx = D; a.dx_chain_stride = 0;
-      } else {
-        a.dX = stage; a.lddx = D; a.dx_chain_stride = P * D;
-        if (moe_fused(p, true)) { a.combine = dsum; a.counters = reinterpret_cast<int*>(p->P_("moe_cnt")); }
-        a.stage_b16 = moe_stage_b16(p, true) ? 1 : 0;
-      }
+      a.dX = stage; a.lddx = D; a.dx_chain_stride = P * D;
+      a.stage_b16 = moe_stage_b16(p) ? 1 : 0;
       GNOT_RUN(chain_bwd(a, m1 ? p->k_m1(l) : p->k_m2(l), P, m1 ? p->wg_m1[l] : p->wg_m2[l], "moe_bwd"));
-      if (!walk && !moe_fused(p, true)) GNOT_CK(launch_moe_pass(p, nullptr, stage, dsum, c.s));
+      GNOT_CK(launch_moe_pass(p, nullptr, stage, dsum, c.s));
       GNOT_RUN(flush_deferred(c));            // the chain's weight gradients: side launch after the pass
       // m2: self attention (model.py:133) ; m1: cross attention (model.py:127)
       GNOT_RUN(attn_backward(c, l, m1));

@@ -82,7 +82,7 @@ hipError_t launch_linear_batch(const LinearArgs* jobs_dev, int njobs, int maxP, 
 // ------------------------------------------------------------------ fused MLP chains (chain.hip)
 enum ChainMode { CH_STORE = 0, CH_SOFTMAX = 1, CH_MOE = 2 };
 // points per workgroup of the d = 256 chain kernels (chain2.hip: 16 per wave): one block of the soft-MoE
-// expert grid, and one fused-combine completion counter
+// expert grid
 constexpr int kC2Rows = 128;
 struct ChainLayer {
   const float4* Wp;    // packed forward weights of this layer
@@ -113,19 +113,6 @@ struct ChainArgs {
   float* dz; long dz_layer_stride; long dz_chain_stride;          // per layer dZ [P, D] for wgrad
   float* dX; long lddx; long dx_chain_stride;                     // chain input grad or null
   int np = 3;                        // d = 256: operand pieces (3 = bf16x6 fp32-exact, 1 = bf16 mode)
-  // CH_MOE, d = 256 (chain2.hip) "walk" form: ONE workgroup runs every expert of its 128 points in
-  // order and sums in place -- forward Y = base + sum_e s_e * MLP_e(X) (model.py:128-131), backward
-  // dX = sum_e W_e0^T dz_e0 -- so no [P, E, d] stage and no combine pass (grid.y = 1).  Forward Y may
-  // be null (MoE recompute: saves only).
-  int walk = 0;
-  const float* base = nullptr;       // forward: the residual (query in) of the walk form / the fused combine
-  // CH_MOE expert grid (walk = 0), d = 256: the fused soft-MoE combine.  The E workgroups of a 128-point
-  // block store their stage rows write-through and count their completions in counters[block]; the LAST
-  // one sums the block's E stage rows in expert order into `combine` (forward: base + sum_e s_e y_e,
-  // model.py:128-131; backward: d(MoE input) = sum_e dX_e) -- no separate combine pass.  counters: one
-  // int per 128-point block, zero between launches (each launch's last workgroups reset theirs)
-  float* combine = nullptr;
-  int* counters = nullptr;
 #ifdef GNOT_DIAG_STAMP
   unsigned long long* dbg = nullptr;  // diagnostic builds: per-wave stamp sums (x6_core.h C2Pipe)
 #endif
@@ -139,28 +126,14 @@ struct ChainArgs {
   // MFMA operand the forward used), written for the weight gradients; slot nlin + 0 (the shared MoE
   // input) only in chain 0.
   int b16s = 0;
-  // b16s expert grid without the fused combine: the stage terms (forward s_e y_e, backward dX_e) go to the
-  // [E, P, d] stage as bf16 pair-interleaved rows (plain stores; the strides are the fp32 stage's), summed by
-  // launch_moe_combine_b16
+  // b16s expert grid: the stage terms (forward s_e y_e, backward dX_e) go to the [E, P, d] stage as bf16
+  // pair-interleaved rows (the strides are the fp32 stage's), summed by launch_moe_combine_b16
   int stage_b16 = 0;
 };
-// d <= 192 chain backward-data in the fp32 mode: bf16x6 on k-major 3-piece images of W^T (pack x6 = 1), as
-// the forward; -DGNOT_CHAIN_BWD_FP32 builds the round-1..4 form (exact fp32 MFMA on fp32 fragment images)
-#ifdef GNOT_CHAIN_BWD_FP32
-constexpr bool kChainBwdX6 = false;
-#else
-constexpr bool kChainBwdX6 = true;
-#endif
 // d <= 192 projections in the fp32 mode: bf16x6 on output-major 3-piece images (pack x6 = 2), as linear2.hip
-// at d = 256; -DGNOT_LINEAR_FP32 builds the round-1..4 form (exact fp32 MFMA on fp32 fragment images).
+// at d = 256 (round 5; exact fp32 MFMA on fp32 fragment images before -- the form d > 192 keeps).
 // configs[1] (d = 128), one box, interleaved x2: 3.37 / 3.35 ms per step against 3.44 / 3.44 (profiles/r05o*)
-#ifdef GNOT_LINEAR_FP32
-constexpr bool kLinearX6 = false;
-#else
 constexpr bool kLinearX6 = true;
-#endif
-// walk or per-expert grid for a MoE call of P points (env GNOT_MOE_WALK = 0 / 1 forces, read per call)
-bool chain2_walk_choice(long P, int E);
 // d > 256: chains one Linear at a time (linear.hip + elementwise passes, chainw.hip)
 hipError_t launch_chainw(const ChainArgs& a, bool bwd, hipStream_t s);
 hipError_t launch_chain_fwd(const ChainArgs& a, hipStream_t s);

@@ -118,21 +118,6 @@ int main(int argc, char** argv) {
   t = time_us([&] { CK(launch_chain_bwd(bw, nullptr)); });
   std::printf("chain_bwd  MoE E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
   STAMP("chain_bwd MoE x6", bw, true);
-  if (D == 256) {   // the fused soft-MoE combine (counters zero between launches)
-    int* cnt = nullptr;
-    CK(hipMalloc(&cnt, (size_t)P * sizeof(int)));
-    CK(hipMemset(cnt, 0, (size_t)P * sizeof(int)));
-    float* qout = dalloc((size_t)P * D, 0.0f);
-    ChainArgs af = a, bf = bw;
-    af.base = X; af.combine = qout; af.counters = cnt;
-    bf.combine = qout; bf.counters = cnt;
-    t = time_us([&] { CK(launch_chain_fwd(af, nullptr)); });
-    std::printf("chain_fwd  MoE+combine E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
-    t = time_us([&] { CK(launch_chain_bwd(bf, nullptr)); });
-    std::printf("chain_bwd  MoE+combine E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
-    CK(hipFree(qout));
-    CK(hipFree(cnt));
-  }
   if (D == 256) {   // bf16 arithmetic mode (one operand piece)
     ChainArgs a1 = a, b1 = bw;
     a1.np = 1; b1.np = 1;
@@ -145,27 +130,11 @@ int main(int argc, char** argv) {
     a2.b16s = 1; a2.save_layer_stride = (long)P * D / 2; a2.save_chain_stride = (long)NL * P * D;
     b2.b16s = 1; b2.save_layer_stride = a2.save_layer_stride; b2.save_chain_stride = a2.save_chain_stride;
     b2.dz_layer_stride = (long)P * D / 2; b2.dz_chain_stride = (long)NL * P * D / 2;
-    // the bf16 expert terms are summed by the fused combine only; without it, the saves-only forward
-    // (MoE recompute's first pass)
+    // the saves-only forward (MoE recompute's first pass)
     a2.Y = nullptr;
     t = time_us([&] { CK(launch_chain_fwd(a2, nullptr)); });
     std::printf("chain_fwd  b16s saves-only E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
     a2.Y = Y;
-    int* cnt = nullptr;
-    CK(hipMalloc(&cnt, (size_t)P * sizeof(int)));
-    CK(hipMemset(cnt, 0, (size_t)P * sizeof(int)));
-    float* qout = dalloc((size_t)P * D, 0.0f);
-    ChainArgs af = a2, bf = b2;
-    af.base = X; af.combine = qout; af.counters = cnt;
-    bf.combine = qout; bf.counters = cnt;
-    t = time_us([&] { CK(launch_chain_fwd(af, nullptr)); });
-    std::printf("chain_fwd  b16s+combine E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
-    STAMP("chain_fwd b16s+combine", af, false);
-    t = time_us([&] { CK(launch_chain_bwd(bf, nullptr)); });
-    std::printf("chain_bwd  b16s+combine E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
-    STAMP("chain_bwd b16s+combine", bf, true);
-    CK(hipFree(qout));
-    CK(hipFree(cnt));
     // the bf16 mode's default soft-MoE form: bf16 stage rows for the moe_combine_b16 pass
     ChainArgs a3 = a2, b3 = b2;
     a3.stage_b16 = 1; a3.y_chain_stride = (long)P * D / 2;

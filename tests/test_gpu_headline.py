@@ -14,8 +14,7 @@ the 262,144-point bench takes:
   256 workgroups: 6 splits per MoE job group of 40 Linears, 51 per single-chain group of 5), and an
   odd number of 16-point stages in the last split (70,000 - 5 * 11,680 = 11,600 points = 725
   stages), the case of the stage-buffer reuse the db column sums once raced on;
-* the soft-MoE expert grid + moe_combine (the default the bench runs) and the walk form
-  (GNOT_MOE_WALK=1);
+* the soft-MoE expert grid + moe_combine (the form the bench runs);
 * 70,000 is not a multiple of 128 (a partial last chain workgroup) nor of 256 (a partial state block).
 
 Checked against the float64 CPU oracle (oracle/gnot_oracle.py, pinned to the reference fixtures):
@@ -42,18 +41,15 @@ N_MID, M = 70000, 805    # the session fixture mid_case (conftest.py): one 70,00
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("walk", ["1", "0"])
-def test_configs2_widths_70k_points_fp32(mid_case, walk, monkeypatch):
-    """walk "0": the expert grid + moe_combine (the default, chain2_walk_choice); "1": the soft-MoE walk
-    form (GNOT_MOE_WALK=1)."""
-    monkeypatch.setenv("GNOT_MOE_WALK", walk)
+def test_configs2_widths_70k_points_fp32(mid_case):
+    """the expert grid + moe_combine, fp32."""
     fx, G = mid_case
     m = build_model(fx["params"], fx["cfg"])
     out, grads = run_packed(m, fx, G)
     errs = check_parity(out, grads, fx)
     keys = sorted(fx["grads"])
     cat = lambda g: np.concatenate([np.ravel(g[k]) for k in keys])
-    print(f"\n70k fp32 walk={walk}: out rel {rel(out, fx['out']):.3e}, all-grad rel {rel(cat(grads), cat(fx['grads'])):.3e}")
+    print(f"\n70k fp32: out rel {rel(out, fx['out']):.3e}, all-grad rel {rel(cat(grads), cat(fx['grads'])):.3e}")
     assert not errs, errs
     out2, grads2 = run_packed(m, fx, G)
     assert np.array_equal(out, out2)
@@ -62,11 +58,8 @@ def test_configs2_widths_70k_points_fp32(mid_case, walk, monkeypatch):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("walk", ["0", "1"])
-def test_configs2_widths_70k_points_bf16_mode(mid_case, walk, monkeypatch):
-    """bf16 mode at 1e-2 of the fp64 oracle, in the default soft-MoE form the bench runs (walk "0": the
-    expert grid, chain2_walk_choice) and in the walk form (GNOT_MOE_WALK=1)."""
-    monkeypatch.setenv("GNOT_MOE_WALK", walk)
+def test_configs2_widths_70k_points_bf16_mode(mid_case):
+    """bf16 mode at 1e-2 of the fp64 oracle, in the soft-MoE form the bench runs."""
     fx, G = mid_case
     m = build_model(fx["params"], fx["cfg"])
     m.set_precision("bf16")
@@ -74,7 +67,7 @@ def test_configs2_widths_70k_points_bf16_mode(mid_case, walk, monkeypatch):
     keys = sorted(fx["grads"])
     cat = lambda g: np.concatenate([np.ravel(g[k]) for k in keys])
     e_out, e_grad = rel(out, fx["out"]), rel(cat(grads), cat(fx["grads"]))
-    print(f"\n70k bf16 mode walk={walk}: out rel {e_out:.3e}, all-grad rel {e_grad:.3e}")
+    print(f"\n70k bf16 mode: out rel {e_out:.3e}, all-grad rel {e_grad:.3e}")
     assert e_out < 1e-2 and e_grad < 1e-2, (e_out, e_grad)
 
 

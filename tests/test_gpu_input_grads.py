@@ -70,20 +70,17 @@ def _port_grads(cfg, sd64, xs, thetas, fns_per_sample, Gs, autocast=False):
     return gx, gt, gf
 
 
-@pytest.mark.parametrize("name,prec,walk,recompute", [
-    ("d64_I2", "fp32", "0", False),
-    ("d256_I1", "fp32", "0", False),     # the default soft-MoE form (expert grid + combine)
-    ("d256_I1", "fp32", "1", False),     # the walk form (GNOT_MOE_WALK=1)
-    ("d256_I1", "fp32", "0", True),      # MoE recompute
-    ("d256_I1", "bf16", "0", False),     # bf16 mode: bf16-storage MoE chains feeding the encoder backward
-    ("d256_I1", "bf16", "1", False),
-    ("d300_I1", "fp32", "0", False),
-    ("d300_I1", "fp32", "0", True),
-    ("d100_h4_I2", "fp32", "0", False),
+@pytest.mark.parametrize("name,prec,recompute", [
+    ("d64_I2", "fp32", False),
+    ("d256_I1", "fp32", False),          # the soft-MoE expert grid + combine
+    ("d256_I1", "fp32", True),           # MoE recompute
+    ("d256_I1", "bf16", False),          # bf16 mode: bf16-storage MoE chains feeding the encoder backward
+    ("d300_I1", "fp32", False),
+    ("d300_I1", "fp32", True),
+    ("d100_h4_I2", "fp32", False),
 ])
-def test_input_grads_packed_match_port(name, prec, walk, recompute, monkeypatch):
+def test_input_grads_packed_match_port(name, prec, recompute):
     """north_star's bar per arithmetic: 1e-4 in fp32, 1e-2 in bf16 mode."""
-    monkeypatch.setenv("GNOT_MOE_WALK", walk)
     tol = 1e-4 if prec == "fp32" else 1e-2
     cfg, m, sd64 = _setup(name)
     m.set_precision(prec)
@@ -123,7 +120,7 @@ def test_input_grads_packed_match_port(name, prec, walk, recompute, monkeypatch)
     ref = [np.concatenate(rx), np.stack(rt)] + [np.concatenate([rf[b][i] for b in range(len(Ns))]) for i in range(I)]
     errs = [_rel(g, r) for g, r in zip(got, ref)]
     e_all = _rel(np.concatenate([g.ravel() for g in got]), np.concatenate([r.ravel() for r in ref]))
-    print(f"\ninput grads {name} {prec} walk={walk} recompute={recompute}: dx {errs[0]:.2e} dtheta {errs[1]:.2e} "
+    print(f"\ninput grads {name} {prec} recompute={recompute}: dx {errs[0]:.2e} dtheta {errs[1]:.2e} "
           f"dfns {errs[2:]} all {e_all:.2e}")
     # fp32: every input gradient at 1e-4.  bf16 mode: norm-wise over all input gradients concatenated at
     # north_star's 1e-2 (the rule tests/test_gpu_bf16.py applies to the parameter gradients), and per tensor
