@@ -68,9 +68,15 @@ struct WgradGroup {
   std::vector<int> lins;             // weight-gradient groups: the canonical Linears whose (dW, db) they write
   int state_pts = 0, state_nw = 0;
   bool state_mfma = false;   // state groups: points per workgroup, per-point weights (0 or H)
+  // balanced wide groups: per-workgroup point ranges {job, slot, begin, end} (launch_wgrad segs) and the
+  // first range of every workgroup (+ the end)
+  std::vector<int4> segs;
+  std::vector<int> seg_start;
   WgradJob* d_jobs = nullptr;        // device copies (workspace tables)
   int* d_wg_prefix = nullptr;
   int* d_red_prefix = nullptr;
+  int4* d_segs = nullptr;
+  int* d_seg_start = nullptr;
 };
 
 struct ChainTable {
@@ -622,6 +628,14 @@ static void plan_images(gnot_plan* p) {
 // ====================================================================== point-reduction GEMM groups
 // split-K target of the 128-wide kernel
 constexpr long kWide128Wgs = 128;
+// balanced point ranges for a wide group (finish_group) when a per-job split count would leave CUs idle and
+// every job has a point range of its own (no zero-point jobs)
+static bool balanced_wgrad(const WgradGroup& G) {
+  if (G.jobs.size() < 2) return false;
+  for (const auto& J : G.jobs)
+    if (J.P <= 0) return false;
+  return 256 % (long)G.jobs.size() != 0;
+}
 static void finish_group(gnot_plan* p, WgradGroup& G) {
   G.x6 = true;
   for (const auto& J : G.jobs)
@@ -657,7 +671,52 @@ static void finish_group(gnot_plan* p, WgradGroup& G) {
   const long want = std::max<long>(1, target / std::max<long>(tiles, 1));
   G.wg_prefix.clear();
   G.red_prefix.clear();
+  G.segs.clear();
+  G.seg_start.clear();
   G.slab_floats = 0;
+  if (G.wide && G.tw == 256 && !G.b16 && balanced_wgrad(G)) {
+    // the 256 x 256 kernel holds one workgroup per CU: a per-job split count leaves target % jobs CUs idle
+    // (the 40 soft-MoE jobs of configs[2]: 6 splits each = 240 of 256), so cut the group's concatenated
+    // points into `target` equal ranges instead (a range crossing a job boundary runs as two segments)
+    long T = 0, maxrow = 1;
+    for (const auto& J : G.jobs) {
+      T += J.P;
+      maxrow = std::max<long>(maxrow, 4L * std::max<long>(std::max<long>(J.lddz, J.ldx), 1));
+    }
+    long C = std::max<long>((T + target - 1) / target, kMinSplitPoints);
+    C = (C + 15) / 16 * 16;                                 // whole 16-point stages (kWStage)
+    C = std::min<long>(C, ((1L << 31) - 1) / maxrow - 64);  // a range's rows stay below 2^31 bytes
+    std::vector<long> jstart(G.jobs.size() + 1, 0);
+    for (size_t j = 0; j < G.jobs.size(); ++j) jstart[j + 1] = jstart[j] + G.jobs[j].P;
+    std::vector<int> nslots(G.jobs.size(), 0);
+    size_t jj = 0;
+    for (long w0 = 0; w0 < T; w0 += C) {
+      const long w1 = std::min(T, w0 + C);
+      G.seg_start.push_back((int)G.segs.size());
+      while (jj < G.jobs.size() && jstart[jj + 1] <= w0) ++jj;
+      for (size_t j = jj; j < G.jobs.size() && jstart[j] < w1; ++j) {
+        const long b = std::max(w0, jstart[j]) - jstart[j], e = std::min(w1, jstart[j + 1]) - jstart[j];
+        if (e > b) G.segs.push_back(int4{(int)j, nslots[j]++, (int)b, (int)e});
+      }
+    }
+    G.seg_start.push_back((int)G.segs.size());
+    int red = 0;
+    for (size_t j = 0; j < G.jobs.size(); ++j) {
+      auto& J = G.jobs[j];
+      J.splits = std::max(1, nslots[j]);
+      const int nt = J.tiles_o * J.tiles_i;
+      J.slab_off = (long)G.slab_floats;
+      G.slab_floats += (size_t)J.splits * nt * kPTile * (kPTile + 1);
+      G.wg_prefix.push_back(0);
+      G.red_prefix.push_back(red);
+      red += nt * kPTile * (kPTile + 1);
+    }
+    G.total_wgs = (int)G.seg_start.size() - 1;
+    G.total_red = red;
+    size_t& slab = p->slab_wgrad_floats;
+    slab = std::max(slab, G.slab_floats);
+    return;
+  }
   int wg = 0, red = 0;
   for (auto& J : G.jobs) {
     const long minpts = kMinSplitPoints;   // >= 4 LDS stages per workgroup: bounds the split-K slab traffic
@@ -1343,6 +1402,8 @@ extern "C" int gnot_plan_set_batch(gnot_plan* p, int B, const int64_t* x_off, co
   auto tbl_group = [&](const WgradGroup& G) {
     tbl(G.jobs.size() * sizeof(WgradJob));
     tbl(G.jobs.size() * sizeof(int) * 2);
+    tbl(G.segs.size() * sizeof(int4));
+    tbl(G.seg_start.size() * sizeof(int));
   };
   for_each_group(p, tbl_group);
   build_attn_tables(p);
@@ -1472,6 +1533,8 @@ extern "C" int gnot_plan_bind_workspace_async(gnot_plan* p, void* workspace, siz
       int* d = static_cast<int*>(put(pre.data(), pre.size() * sizeof(int)));
       G.d_wg_prefix = d;
       G.d_red_prefix = d + G.jobs.size();
+      G.d_segs = G.segs.empty() ? nullptr : static_cast<int4*>(put(G.segs.data(), G.segs.size() * sizeof(int4)));
+      G.d_seg_start = G.segs.empty() ? nullptr : static_cast<int*>(put(G.seg_start.data(), G.seg_start.size() * sizeof(int)));
     });
   }
   build_attn_tables(p);
@@ -1669,7 +1732,7 @@ int launch_group(gnot_plan* p, const WgradGroup& G, float* slab, hipStream_t s) 
                              slab, s));
   else
     GNOT_CK(launch_wgrad(G.d_jobs, G.d_wg_prefix, (int)G.jobs.size(), G.total_wgs, G.d_red_prefix, G.total_red, slab,
-                         s, G.x6, G.wide, p->npk(), G.tw));
+                         s, G.x6, G.wide, p->npk(), G.tw, G.d_segs, G.d_seg_start));
   return GNOT_OK;
 }
 

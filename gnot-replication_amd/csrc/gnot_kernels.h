@@ -166,9 +166,13 @@ struct WgradJob {
 // wide: the same on the 256 x 256-tile kernel (out, in <= 256; ONE workgroup per (job, split), so
 //       wg_prefix counts splits only)
 // tw: the wide kernel's output edge, 256 (d = 256) or 128 (d <= 128: every job within 128 x 128)
+// segs / seg_start (wide kernel only, optional): the balanced form -- workgroup w runs the point ranges
+// segs[seg_start[w] .. seg_start[w+1]) = {job, slab slot, first point, end point}; each job's J.splits
+// then counts the ranges that touch it (slots 0 .. splits-1)
 hipError_t launch_wgrad(const WgradJob* jobs_dev, const int* wg_prefix_dev, int njobs, int total_wgs,
                         const int* red_prefix_dev, int total_red, float* slab, hipStream_t s, bool x6 = false,
-                        bool wide = false, int np = 3, int tw = 256);   // np: operand pieces (1 = bf16 mode)
+                        bool wide = false, int np = 3, int tw = 256,    // np: operand pieces (1 = bf16 mode)
+                        const int4* segs = nullptr, const int* seg_start = nullptr);
 // bf16-storage jobs (ChainArgs::b16s): dz and x point at bf16 pair-interleaved rows [P, 256] (x already
 // the Linear's input, no GELU), out = in = 256, one workgroup per (job, split) as the wide kernel
 hipError_t launch_wgrad_b16(const WgradJob* jobs_dev, const int* wg_prefix_dev, int njobs, int total_wgs,

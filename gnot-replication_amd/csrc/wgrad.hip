@@ -405,10 +405,16 @@ GNOT_DEV float lds_read_b32_off(unsigned addr) {
   return v;
 }
 
+// segs / seg_start (balanced groups, engine.cpp finish_group): workgroup w runs the point ranges
+// segs[seg_start[w] .. seg_start[w + 1]) = {job, slab slot, first point, end point} one after the other (a
+// range of the groups' concatenated points, cut at job boundaries), so every workgroup gets the same share
+// of the group's points whatever the job count; without them, one split of one job (prefix)
 template <int NP = 3, int TW = 256>
 __global__ void __launch_bounds__(w_threads(TW)) pgemm_x6w_kernel(const WgradJob* __restrict__ jobs,
                                                                  const int* __restrict__ prefix, int njobs,
-                                                                 float* __restrict__ slab) {
+                                                                 float* __restrict__ slab,
+                                                                 const int4* __restrict__ segs,
+                                                                 const int* __restrict__ seg_start) {
   constexpr int NW = TW / 32;            // waves
   constexpr int FG = TW / 64;            // 64-feature groups of the raw-row DMA
   constexpr int WC = NW / 2;             // waves along the columns
@@ -417,12 +423,23 @@ __global__ void __launch_bounds__(w_threads(TW)) pgemm_x6w_kernel(const WgradJob
   extern __shared__ __attribute__((aligned(16))) u32x4 wl[];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int j = find_job(prefix, njobs, blockIdx.x);
+  int k0 = 0, k1 = 1;
+  if (segs != nullptr) { k0 = seg_start[blockIdx.x]; k1 = seg_start[blockIdx.x + 1]; }
+  for (int kseg = k0; kseg < k1; ++kseg) {
+  int j, split;
+  long pb, pe;
+  if (segs != nullptr) {
+    const int4 sg = segs[kseg];
+    j = sg.x; split = sg.y; pb = sg.z; pe = sg.w;
+    if (kseg > k0) __syncthreads();      // the previous range's LDS readers are done (its DMAs have landed)
+  } else {
+    j = find_job(prefix, njobs, blockIdx.x);
+    split = blockIdx.x - prefix[j];
+    const int chunk = ((jobs[j].P + jobs[j].splits - 1) / jobs[j].splits + kWStage - 1) / kWStage * kWStage;
+    pb = (long)split * chunk;
+    pe = min((long)jobs[j].P, pb + chunk);
+  }
   const WgradJob J = jobs[j];
-  const int split = blockIdx.x - prefix[j];
-  const int chunk = ((J.P + J.splits - 1) / J.splits + kWStage - 1) / kWStage * kWStage;
-  const long pb = (long)split * chunk;
-  const long pe = min((long)J.P, pb + chunk);
   const int nst = pe > pb ? (int)((pe - pb + kWStage - 1) / kWStage) : 0;
   // staging role (the point half hh is wave-uniform: waves 0 .. NW/2-1 / NW/2 ..)
   const int f = tid & (TW - 1), hh = tid / TW;
@@ -660,6 +677,7 @@ __global__ void __launch_bounds__(w_threads(TW)) pgemm_x6w_kernel(const WgradJob
     if (tid < TW && f < J.out)
       S0[((f >> 7) * J.tiles_i) * (kTile * (kTile + 1)) + (f & 127) * (kTile + 1) + kTile] = red[f] + red[TW + f];
   }
+  }
 }
 
 // ---------------------------------------------------------------- bf16-storage variant (bf16 mode)
@@ -868,7 +886,7 @@ hipError_t launch_wgrad_b16(const WgradJob* jobs_dev, const int* wg_prefix_dev, 
 
 hipError_t launch_wgrad(const WgradJob* jobs_dev, const int* wg_prefix_dev, int njobs, int total_wgs,
                         const int* red_prefix_dev, int total_red, float* slab, hipStream_t s, bool x6, bool wide,
-                        int np, int tw) {
+                        int np, int tw, const int4* segs, const int* seg_start) {
   if (njobs <= 0) return hipSuccess;
   if (wide) {
     const size_t lds = w_lds_bytes(np, tw);
@@ -881,7 +899,7 @@ hipError_t launch_wgrad(const WgradJob* jobs_dev, const int* wg_prefix_dev, int 
       attr = true;                                                                                             \
     }                                                                                                          \
     hipLaunchKernelGGL((pgemm_x6w_kernel<NP_, TW_>), dim3(total_wgs), dim3(w_threads(TW_)), lds, s, jobs_dev,  \
-                       wg_prefix_dev, njobs, slab);                                                            \
+                       wg_prefix_dev, njobs, slab, segs, seg_start);                                           \
   }
     GNOT_X6W(3, 256) GNOT_X6W(1, 256) GNOT_X6W(3, 128) GNOT_X6W(1, 128)
 #undef GNOT_X6W
