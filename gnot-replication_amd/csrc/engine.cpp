@@ -674,17 +674,17 @@ static void finish_group(gnot_plan* p, WgradGroup& G) {
   G.segs.clear();
   G.seg_start.clear();
   G.slab_floats = 0;
-  if (G.wide && G.tw == 256 && !G.b16 && balanced_wgrad(G)) {
+  if (G.wide && G.tw == 256 && balanced_wgrad(G)) {
     // the 256 x 256 kernel holds one workgroup per CU: a per-job split count leaves target % jobs CUs idle
     // (the 40 soft-MoE jobs of configs[2]: 6 splits each = 240 of 256), so cut the group's concatenated
     // points into `target` equal ranges instead (a range crossing a job boundary runs as two segments)
     long T = 0, maxrow = 1;
     for (const auto& J : G.jobs) {
       T += J.P;
-      maxrow = std::max<long>(maxrow, 4L * std::max<long>(std::max<long>(J.lddz, J.ldx), 1));
+      maxrow = std::max<long>(maxrow, G.b16 ? 512L : 4L * std::max<long>(std::max<long>(J.lddz, J.ldx), 1));
     }
     long C = std::max<long>((T + target - 1) / target, kMinSplitPoints);
-    C = (C + 15) / 16 * 16;                                 // whole 16-point stages (kWStage)
+    C = (C + 31) / 32 * 32;                                 // whole stages (kWStage 16, kBStage 32 points)
     C = std::min<long>(C, ((1L << 31) - 1) / maxrow - 64);  // a range's rows stay below 2^31 bytes
     std::vector<long> jstart(G.jobs.size() + 1, 0);
     for (size_t j = 0; j < G.jobs.size(); ++j) jstart[j + 1] = jstart[j] + G.jobs[j].P;
@@ -1729,7 +1729,7 @@ int guard_write(Ctx& c, const float* buf) {
 int launch_group(gnot_plan* p, const WgradGroup& G, float* slab, hipStream_t s) {
   if (G.b16)
     GNOT_CK(launch_wgrad_b16(G.d_jobs, G.d_wg_prefix, (int)G.jobs.size(), G.total_wgs, G.d_red_prefix, G.total_red,
-                             slab, s));
+                             slab, s, G.d_segs, G.d_seg_start));
   else
     GNOT_CK(launch_wgrad(G.d_jobs, G.d_wg_prefix, (int)G.jobs.size(), G.total_wgs, G.d_red_prefix, G.total_red, slab,
                          s, G.x6, G.wide, p->npk(), G.tw, G.d_segs, G.d_seg_start));

@@ -176,7 +176,8 @@ hipError_t launch_wgrad(const WgradJob* jobs_dev, const int* wg_prefix_dev, int 
 // bf16-storage jobs (ChainArgs::b16s): dz and x point at bf16 pair-interleaved rows [P, 256] (x already
 // the Linear's input, no GELU), out = in = 256, one workgroup per (job, split) as the wide kernel
 hipError_t launch_wgrad_b16(const WgradJob* jobs_dev, const int* wg_prefix_dev, int njobs, int total_wgs,
-                            const int* red_prefix_dev, int total_red, float* slab, hipStream_t s);
+                            const int* red_prefix_dev, int total_red, float* slab, hipStream_t s,
+                            const int4* segs = nullptr, const int* seg_start = nullptr);
 
 // ------------------------------------------------------------------ attention states (state.hip)
 // Jobs are WgradJobs with state_dh > 0: A = dz/lddz, B = x/ldx, optional w/ldw, out = dW as

@@ -705,18 +705,31 @@ GNOT_DEV u32x2 lds_tr_b64(unsigned addr) {
   return v;
 }
 
+// segs / seg_start: the balanced point ranges of pgemm_x6w_kernel
 __global__ void __launch_bounds__(kWThreads) pgemm_b16_kernel(const WgradJob* __restrict__ jobs,
                                                              const int* __restrict__ prefix, int njobs,
-                                                             float* __restrict__ slab) {
+                                                             float* __restrict__ slab, const int4* __restrict__ segs,
+                                                             const int* __restrict__ seg_start) {
   extern __shared__ __attribute__((aligned(16))) u32x4 bl[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int j = find_job(prefix, njobs, blockIdx.x);
+  int k0 = 0, k1 = 1;
+  if (segs != nullptr) { k0 = seg_start[blockIdx.x]; k1 = seg_start[blockIdx.x + 1]; }
+  for (int kseg = k0; kseg < k1; ++kseg) {
+  int j, split;
+  long pb, pe;
+  if (segs != nullptr) {
+    const int4 sg = segs[kseg];
+    j = sg.x; split = sg.y; pb = sg.z; pe = sg.w;
+    if (kseg > k0) __syncthreads();      // every wave is done with the previous range's stage slots
+  } else {
+    j = find_job(prefix, njobs, blockIdx.x);
+    split = blockIdx.x - prefix[j];
+    const int chunk = ((jobs[j].P + jobs[j].splits - 1) / jobs[j].splits + kBStage - 1) / kBStage * kBStage;
+    pb = (long)split * chunk;
+    pe = min((long)jobs[j].P, pb + chunk);
+  }
   const WgradJob J = jobs[j];
-  const int split = blockIdx.x - prefix[j];
-  const int chunk = ((J.P + J.splits - 1) / J.splits + kBStage - 1) / kBStage * kBStage;
-  const long pb = (long)split * chunk;
-  const long pe = min((long)J.P, pb + chunk);
   const int nst = pe > pb ? (int)((pe - pb + kBStage - 1) / kBStage) : 0;
   const int wr = wave >> 2, wc = wave & 3;
   // resources based at the split's first row: rows past the split read 0 (only the last split's last
@@ -819,6 +832,7 @@ __global__ void __launch_bounds__(kWThreads) pgemm_b16_kernel(const WgradJob* __
     const int f = wr * 128 + wc * 32 + lane;
     S0[((f >> 7) * J.tiles_i) * (kTile * (kTile + 1)) + (f & 127) * (kTile + 1) + kTile] = dbacc;
   }
+  }
 }
 
 // sum the split partials; normal jobs write dW[out, in] (+ db[out]); state jobs (state_dh > 0) write
@@ -870,7 +884,8 @@ __global__ void __launch_bounds__(256) pgemm_reduce_kernel(const WgradJob* __res
 }
 
 hipError_t launch_wgrad_b16(const WgradJob* jobs_dev, const int* wg_prefix_dev, int njobs, int total_wgs,
-                            const int* red_prefix_dev, int total_red, float* slab, hipStream_t s) {
+                            const int* red_prefix_dev, int total_red, float* slab, hipStream_t s, const int4* segs,
+                            const int* seg_start) {
   if (njobs <= 0) return hipSuccess;
   static bool attr = false;
   if (!attr) {
@@ -878,7 +893,8 @@ hipError_t launch_wgrad_b16(const WgradJob* jobs_dev, const int* wg_prefix_dev, 
                               (int)kBLds);
     attr = true;
   }
-  hipLaunchKernelGGL(pgemm_b16_kernel, dim3(total_wgs), dim3(kWThreads), kBLds, s, jobs_dev, wg_prefix_dev, njobs, slab);
+  hipLaunchKernelGGL(pgemm_b16_kernel, dim3(total_wgs), dim3(kWThreads), kBLds, s, jobs_dev, wg_prefix_dev, njobs, slab,
+                     segs, seg_start);
   hipLaunchKernelGGL(pgemm_reduce_kernel, dim3((total_red + 255) / 256), dim3(256), 0, s, jobs_dev, red_prefix_dev,
                      njobs, total_red, (const float*)slab);
   return hipGetLastError();
