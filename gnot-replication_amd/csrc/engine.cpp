@@ -345,10 +345,6 @@ extern "C" int gnot_plan_create(const gnot_config* cfg, gnot_plan** out) {
     return fail(GNOT_E_INVALID, "hidden width must be at most 512 on the MI355X kernels");
   if (D > 256 && 64 % dh != 0)
     return fail(GNOT_E_INVALID, "above hidden width 256 the head width must divide 64 on the MI355X kernels");
-  // the VALU attention-state kernel (state.hip state_partial) gives each of its 256 threads at most
-  // kMaxBlk = 4 of the H (dh/4)^2 = d dh / 16 output blocks: always true up to d = 256 (d dh <= 16384)
-  if (c.n_head * dh * dh > 16384)
-    return fail(GNOT_E_INVALID, "d * (d / n_head) must be at most 16384 on the MI355X kernels (attention states)");
   if (dh % 4 != 0 || dh > 64)
     return fail(GNOT_E_INVALID, "head width d/n_head must be a multiple of 4 up to 64 on the MI355X kernels");
   // the projections' fused feature softmax needs whole heads per workgroup: linear2.hip (d = 256) takes

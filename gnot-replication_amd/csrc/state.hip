@@ -28,7 +28,6 @@ GNOT_DEV int find_job_s(const int* __restrict__ prefix, int njobs, int idx) {
   return lo;
 }
 
-constexpr int kMaxBlk = 4;   // 4x4 output blocks per thread: H*(dh/4)^2 = d*dh/16 <= 1024 (gnot_plan_create: d*dh <= 16384)
 // floats of one row-stage region: pts * d rounded up to whole 64-lane x 16-byte DMA instructions
 // (d > 128 takes pts = 8192 / d, e.g. 56 points x 144 = 8,064 floats: 31.5 instructions)
 __host__ __device__ constexpr int state_stage_floats(int pts, int d) { return (pts * d + 255) / 256 * 256; }
@@ -79,8 +78,10 @@ __global__ void __launch_bounds__(kStateThreads) state_partial_kernel(const Wgra
   const int R = nblk >= kStateThreads ? 1 : kStateThreads / nblk;
   const int r = tid / (nblk < kStateThreads ? nblk : kStateThreads);
   float keep[20];
-#pragma unroll
-  for (int k = 0; k < kMaxBlk; ++k) {
+  // 4x4 output blocks per thread: ceil(H (dh/4)^2 / 256) of them (d dh / 4096; round 5 capped this at 4, i.e.
+  // d dh <= 16384, which refused d = 512 with heads of 64)
+  const int nk = nblk >= kStateThreads ? (nblk + kStateThreads - 1) / kStateThreads : 1;
+  for (int k = 0; k < nk; ++k) {
     const int blk = (nblk >= kStateThreads ? tid + k * kStateThreads : tid % nblk);
     const bool active = (nblk >= kStateThreads) ? blk < nblk : (k == 0 && r < R);
     f32x4 acc[4] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f},

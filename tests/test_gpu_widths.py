@@ -54,9 +54,13 @@ CASES = {
     "d21_h7": _cfg(21, 7, 2, 0),          # dh 3 -> 4, kernels at d = 32
     "d150_h6": _cfg(150, 6, 2, 1),        # dh 25 -> 28: H dh' = 168 > 160, kernels at d = 176
     # d > 256: the chains one Linear at a time (chainw.hip) on the fp32-MFMA projection kernel
-    "d320_h10": _cfg(320, 10, 2, 1),      # dh 32 (d * dh <= 16384: the VALU state kernel's block budget)
+    "d320_h10": _cfg(320, 10, 2, 1),      # dh 32
     "d288_h18": _cfg(288, 18, 3, 0, nl=2),  # dh 16, padded to 320, self-attention only
     "d512_h16": _cfg(512, 16, 2, 1),      # dh 32, the widest
+    # heads of 64 above 256: d * dh = 20,480 / 32,768 (round 5 refused d * dh > 16,384: the VALU state kernel
+    # now loops over any number of its 4 x 4 blocks per thread); H = 8 also runs the MFMA state kernel
+    "d320_h5": _cfg(320, 5, 2, 1),
+    "d512_h8": _cfg(512, 8, 2, 1),
 }
 
 
