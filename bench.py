@@ -403,10 +403,10 @@ def main():
                                   "n_attn_hidden_dim", "n_mlp_num_layers", "n_mlp_hidden_dim",
                                   "n_input_hidden_dim", "n_expert", "n_head", "n_input_functions")]).to(device)
     shard = bool(w.get("shard") or w.get("shard_weak")) and (world > 1 or force_shard)
-    # the point-shard exchanges run inside the engine's launch sequence (RCCL through callbacks on the
-    # engine's stream): RCCL kernels are graph-capturable, so the sharded step is captured too; the
-    # host-staged gloo rehearsal stays eager
-    use_graph = not args.no_graph and not (shard and backend != "nccl")
+    # the point-shard exchanges and the per-group gradient all-reduces run inside the engine's launch sequence
+    # (RCCL through callbacks on the engine's stream): RCCL kernels are graph-capturable, so the multi-rank
+    # step is captured too; the host-staged gloo rehearsal stays eager
+    use_graph = not args.no_graph and not ((world > 1 or shard) and backend != "nccl")
     from gnot_amd import train as gtrain
     # main.py:50-51 AdamW(lr=1e-3): one native update over the flat parameter arena (gnot_adamw_step),
     # or torch's fused multi-tensor AdamW (--torch-adamw; capturable keeps its step count on device)
@@ -617,8 +617,9 @@ def main():
             eng.profile_enable(rkind)
             g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             print("[bench] capturing", file=sys.stderr, flush=True)
-            if comm is not None and os.environ.get("GNOT_BENCH_FAIL_CAPTURE") == "1":
-                comm.fail_next_captured = True        # test knob: one collective callback fails mid-capture
+            if comm is not None and int(os.environ.get("GNOT_BENCH_FAIL_CAPTURE", "0")) > 0:
+                # test knob: the n-th collective callback issued under capture fails (1: the forward's first)
+                comm.fail_next_captured = int(os.environ["GNOT_BENCH_FAIL_CAPTURE"])
             try:
                 with torch.cuda.graph(g_fb):
                     fwd_bwd()

@@ -1994,8 +1994,38 @@ static int moe_forward(Ctx& c, const ChainTable& T, const float* in, const float
   return GNOT_OK;
 }
 
+// A call that fails part-way through a stream capture (e.g. a collective callback refused) leaves the side
+// streams it forked into the capture unjoined, and hipStreamEndCapture then fails with "unjoined work" and
+// leaves the caller's stream capturing.  Every side stream still in the capture joins the caller's stream
+// again before the error returns, so the capture ends (the caller discards the graph); eager calls skip it.
+static void rejoin_side_streams(gnot_plan* p, hipStream_t origin) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(origin, &st) != hipSuccess || st != hipStreamCaptureStatusActive) return;
+  for (hipStream_t s : {p->side, p->side2, p->comm_stream}) {
+    hipStreamCaptureStatus ss = hipStreamCaptureStatusNone;
+    if (!s || hipStreamIsCapturing(s, &ss) != hipSuccess || ss != hipStreamCaptureStatusActive) continue;
+    hipEvent_t e = next_event(p);
+    if (hipEventRecord(e, s) == hipSuccess) (void)hipStreamWaitEvent(origin, e, 0);
+  }
+}
+
+static int forward_impl(gnot_plan* p, const float* x, const float* theta, const float* const* fns, float* out,
+                        void* stream);
+static int backward_impl(gnot_plan* p, const float* dout, void* stream);
 extern "C" int gnot_forward(gnot_plan* p, const float* x, const float* theta, const float* const* fns,
                             float* out, void* stream) {
+  const int rc = forward_impl(p, x, theta, fns, out, stream);
+  if (rc != GNOT_OK && p) rejoin_side_streams(p, static_cast<hipStream_t>(stream));
+  return rc;
+}
+extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
+  const int rc = backward_impl(p, dout, stream);
+  if (rc != GNOT_OK && p) rejoin_side_streams(p, static_cast<hipStream_t>(stream));
+  return rc;
+}
+
+static int forward_impl(gnot_plan* p, const float* x, const float* theta, const float* const* fns, float* out,
+                        void* stream) {
   if (!p || !p->ws_bound) return fail(GNOT_E_STATE, "bind_workspace first");
   if (!p->packed) return fail(GNOT_E_STATE, "gnot_pack_weights must run before gnot_forward");
   if (!x || !theta || !out || (p->I > 0 && !fns)) return fail(GNOT_E_INVALID, "null input");
@@ -2087,7 +2117,7 @@ extern "C" int gnot_forward(gnot_plan* p, const float* x, const float* theta, co
   return GNOT_OK;
 }
 
-extern "C" int gnot_backward(gnot_plan* p, const float* dout, void* stream) {
+static int backward_impl(gnot_plan* p, const float* dout, void* stream) {
   if (!p || !p->ws_bound || !p->fwd_done) return fail(GNOT_E_STATE, "gnot_forward must run before gnot_backward");
   if (!p->training) return fail(GNOT_E_STATE, "plan was set up with training = 0");
   if (!dout) return fail(GNOT_E_INVALID, "null dout");

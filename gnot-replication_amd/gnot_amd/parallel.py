@@ -88,7 +88,7 @@ class PointShardComm:
         self.world = dist.get_world_size(group)
         self.stage = stage_via_host
         self.ws = None                        # the engine's uint8 workspace tensor (set by Engine)
-        self.fail_next_captured = False       # test knob: the next collective issued under capture fails
+        self.fail_next_captured = 0           # test knob: the n-th collective issued under capture fails (0: off)
         self._ar = _lib.ALLREDUCE_FN(self._allreduce)
         self._a2a = _lib.ALLTOALLV_FN(self._alltoallv)
         self.struct = _lib.GnotComm(None, self._ar, self._a2a)
@@ -110,9 +110,10 @@ class PointShardComm:
         return torch.cuda.stream(torch.cuda.ExternalStream(int(stream), device=self.ws.device))
 
     def _injected_failure(self):
-        if self.fail_next_captured and torch.cuda.is_current_stream_capturing():
-            self.fail_next_captured = False
-            raise RuntimeError("injected collective failure under capture (PointShardComm.fail_next_captured)")
+        if self.fail_next_captured > 0 and torch.cuda.is_current_stream_capturing():
+            self.fail_next_captured -= 1
+            if self.fail_next_captured == 0:
+                raise RuntimeError("injected collective failure under capture (PointShardComm.fail_next_captured)")
 
     def _allreduce(self, user, buf, count, stream):
         try:
@@ -145,6 +146,7 @@ class PointShardComm:
             rc = [int(recv_counts[i]) for i in range(self.world)]
             dev = self.ws.device
             with self._on(stream):
+                self._injected_failure()
                 s = self._view(send, sum(sc)) if sum(sc) else torch.empty(0, device=dev)
                 r = self._view(recv, sum(rc)) if sum(rc) else torch.empty(0, device=dev)
                 if self.stage:
