@@ -379,10 +379,18 @@ GNOT_DEV unsigned bf16_rne_bits(float x) {
   const unsigned u = f2u(x);
   return (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;
 }
+// RNE bf16 of two floats in one word: ONE v_cvt_pk_bf16_f32, the bits of bf16_rne_bits for finite values (round
+// 6: the one-piece operand splits used bf16_rne_bits, five VALU per element -- 16 % of the bf16-mode chain
+// forward's VALU stream -- for the same bits)
+GNOT_DEV unsigned pk_bf16(float lo, float hi) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  const bf16x2 v = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(unsigned, v);
+}
 // 8 floats -> 8 RNE bf16 (4 dwords, element j in the low half of dword j/2 for even j)
 GNOT_DEV void split8_bf16(const float (&v)[8], u32x4 (&p)[1]) {
 #pragma unroll
-  for (int d = 0; d < 4; ++d) p[0][d] = (bf16_rne_bits(v[2 * d + 1]) << 16) | bf16_rne_bits(v[2 * d]);
+  for (int d = 0; d < 4; ++d) p[0][d] = pk_bf16(v[2 * d], v[2 * d + 1]);
 }
 // NP = 3: the exact bf16x6 split; NP = 1: RNE bf16
 template <int NP>
@@ -404,7 +412,7 @@ GNOT_DEV void split2_np(float v0, float v1, u32x4 (&p)[NP], int d) {
     p[1][d] = pack_hi16(b1, a1);
     p[2][d] = pack_hi16(b2, a2);
   } else {
-    p[0][d] = (bf16_rne_bits(v1) << 16) | bf16_rne_bits(v0);
+    p[0][d] = pk_bf16(v0, v1);
   }
 }
 
@@ -417,12 +425,6 @@ GNOT_DEV void split2_np(float v0, float v1, u32x4 (&p)[NP], int d) {
 constexpr int kB16Row = 512;
 GNOT_DEV int b16_off(int T, int g) { return ((T >> 1) * 4 + g) * 16 + (T & 1) * 8; }
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-// RNE bf16 of two floats in one word (v_cvt_pk_bf16_f32: the bits of bf16_rne_bits for finite values)
-GNOT_DEV unsigned pk_bf16(float lo, float hi) {
-  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-  const bf16x2 v = {(__bf16)lo, (__bf16)hi};
-  return __builtin_bit_cast(unsigned, v);
-}
 GNOT_DEV float bf16_lo(unsigned w) { return u2f(w << 16); }
 GNOT_DEV float bf16_hi(unsigned w) { return u2f(w & 0xFFFF0000u); }
 // 8-byte buffer store (whole offset in the VGPR, soffset 0: see buf_store_f32x4)
