@@ -112,6 +112,12 @@ int main(int argc, char** argv) {
   t = time_us([&] { CK(launch_chain_fwd(a, nullptr)); });
   std::printf("chain_fwd  MoE E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
   STAMP("chain_fwd MoE x6", a, false);
+  {  // the same chains without the training saves (inference form)
+    ChainArgs an = a;
+    an.save = nullptr;
+    t = time_us([&] { CK(launch_chain_fwd(an, nullptr)); });
+    std::printf("chain_fwd  MoE no-save E=%d P=%d D=%d: %8.2f us  %6.1f TFLOP/s\n", E, P, D, t, fl / t / 1e6);
+  }
   ChainArgs bw = a;
   bw.dY = X; bw.lddy = D; bw.dscore = dscore; bw.dz = dz; bw.dz_layer_stride = (long)P * D;
   bw.dz_chain_stride = (long)NL * P * D; bw.dX = dX; bw.lddx = D; bw.dx_chain_stride = (long)P * D;
