@@ -16,7 +16,8 @@
 // segment of one sample, grid.y splits the segment's (point, head, lane) tasks into 256-thread
 // workgroups -> ~8x more waves than one thread per (point, head), which is what the chip needs at
 // 10k-point meshes (the per-thread dependent FMA chains were latency-bound).  The (S, z) states are
-// read through the L1/L2 (every group of one head reads the same 1 KiB).
+// read through the L1/L2 (every group of one head reads the same 1 KiB).  Heads wider than 64 run the
+// wide forms below (16 lanes per head, 4-feature quads dealt round-robin).
 //
 //   attn_apply_fwd  res (head-major)
 //   attn_apply_bwd  du_i, dden_i per source, d(pre-softmax q)
@@ -314,6 +315,266 @@ __global__ void __launch_bounds__(256) attn_kv_bwd_batch_kernel(const AttnKVBwdA
   attn_kv_bwd_body<DH>(a, a.chunks[blockIdx.x]);
 }
 
+// ---------------------------------------------------------------- wide heads (64 < dh <= 256)
+// A 16-lane group per (point, head); lane q owns the 4-feature quads q, q + 16, q + 32, ... of the head
+// (features 64 b + 4 q .. +3 for b < NB = ceil(dh / 64); a quad at or past dh is not owned), so every 64-row
+// block of a state reduces with one 16-lane reduce-scatter (group_reduce_scatter<16, 4>) that lands row
+// 64 b + 4 q + j in the lane that owns feature 64 b + 4 q + j.  The q / k row is read 4 features at a time
+// through the L1 (the group shares it) instead of being held whole in registers as above: 2 dh floats per
+// lane do not fit beside the rest at dh = 256.  dh is a runtime multiple of 4; the per-column k order of
+// the sums is the narrow kernels'.
+constexpr int kWideG = 16;
+
+template <int NB>
+struct WideSlice {
+  int q, dh;
+  GNOT_DEV bool own(int b) const { return 64 * b + 4 * q < dh; }
+  GNOT_DEV int f(int b) const { return 64 * b + 4 * q; }
+};
+
+template <int NB>
+GNOT_DEV void wide_load(float (&v)[NB][4], const float* __restrict__ row, const WideSlice<NB>& w) {
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const float4 x = w.own(b) ? *reinterpret_cast<const float4*>(row + w.f(b)) : make_float4(0.f, 0.f, 0.f, 0.f);
+    v[b][0] = x.x; v[b][1] = x.y; v[b][2] = x.z; v[b][3] = x.w;
+  }
+}
+
+template <int NB>
+GNOT_DEV void wide_store(float* __restrict__ row, const float (&v)[NB][4], const WideSlice<NB>& w) {
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+    if (w.own(b)) *reinterpret_cast<float4*>(row + w.f(b)) = make_float4(v[b][0], v[b][1], v[b][2], v[b][3]);
+}
+
+template <int NB>
+GNOT_DEV float wide_dot(const float (&x)[NB][4], const float (&y)[NB][4]) {
+  float d = 0.f;
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) d = fmaf(x[b][c], y[b][c], d);
+  return d;
+}
+
+template <int NB>
+GNOT_DEV void wide_zero(float (&v)[NB][4]) {
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) v[b][c] = 0.f;
+}
+
+// one pass over rows [64 kb, 64 kb + 64) of a state M (pitch dh): acc[b][c] += x[k] M[k][f(b) + c] (the lane's
+// columns) and rows[j] = sum over the whole group of y . M[64 kb + 4 q + j][:] (the lane's rows)
+template <int NB>
+GNOT_DEV void wide_rows(const float* __restrict__ M, const float* __restrict__ xrow, const float (&y)[NB][4], int kb,
+                        const WideSlice<NB>& w, float (&acc)[NB][4], float (&rows)[4]) {
+  float part[64];
+#pragma unroll
+  for (int i4 = 0; i4 < 16; ++i4) {
+    const int k0 = 64 * kb + 4 * i4;
+    if (k0 < w.dh) {
+      const float4 x4 = *reinterpret_cast<const float4*>(xrow + k0);
+      const float xk[4] = {x4.x, x4.y, x4.z, x4.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float sr[NB][4];
+        wide_load(sr, M + (long)(k0 + r) * w.dh, w);
+        float pk = 0.f;
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            acc[b][c] = fmaf(xk[r], sr[b][c], acc[b][c]);
+            pk = fmaf(y[b][c], sr[b][c], pk);
+          }
+        part[4 * i4 + r] = pk;
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) part[4 * i4 + r] = 0.f;
+    }
+  }
+  group_reduce_scatter<kWideG, 4>(part, w.q);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) rows[j] = part[j];
+}
+
+template <int NB>
+__global__ void __launch_bounds__(256) attn_apply_fwd_wide_kernel(AttnApplyArgs a) {
+  const int4 ch = a.chunks[blockIdx.x];
+  Task t;
+  if (!decode_task<kWideG>(ch, a.H, t)) return;
+  const int dh = a.dh;
+  const long ph = (long)dh * dh + dh;
+  const WideSlice<NB> w{t.q, dh};
+  const int sb = ch.x;
+  const long off_b = a.off[sb];
+  const long Nb = a.off[sb + 1] - off_b;
+  const float* qrow = a.q + t.n * a.ldq + (long)t.h * dh;
+  float qs[NB][4], os[NB][4];
+  wide_load(qs, qrow, w);
+  wide_zero(os);
+  for (int s = 0; s < a.nsrc; ++s) {
+    const float* S = a.state[s] + (long)sb * a.H * ph + t.h * ph;
+    float zs[NB][4], u[NB][4];
+    wide_load(zs, S + (long)dh * dh, w);
+    const float den = group_sum<kWideG>(wide_dot(qs, zs));
+    wide_zero(u);
+    for (int k0 = 0; k0 < dh; k0 += 4) {
+      const float4 q4 = *reinterpret_cast<const float4*>(qrow + k0);
+      const float qk[4] = {q4.x, q4.y, q4.z, q4.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float sr[NB][4];
+        wide_load(sr, S + (long)(k0 + r) * dh, w);
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) u[b][c] = fmaf(qk[r], sr[b][c], u[b][c]);
+      }
+    }
+    const float inv = 1.0f / den;
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) os[b][c] = fmaf(u[b][c], inv, os[b][c]);
+  }
+  const float inv_nsrc = 1.0f / (float)a.nsrc;
+  float r[NB][4];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) r[b][c] = fmaf(os[b][c], inv_nsrc, qs[b][c]);
+  if (a.dhr == 0) {
+    wide_store(a.res + off_b * (long)a.H * dh + ((long)t.h * Nb + (t.n - off_b)) * dh, r, w);
+  } else {
+    float* dst = a.res + off_b * (long)a.H * a.dhr + ((long)t.h * Nb + (t.n - off_b)) * a.dhr;
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (w.f(b) + c < a.dhr) dst[w.f(b) + c] = r[b][c];
+  }
+}
+
+template <int NB>
+__global__ void __launch_bounds__(256) attn_apply_bwd_wide_kernel(AttnApplyArgs a) {
+  const int4 ch = a.chunks[blockIdx.x];
+  Task t;
+  if (!decode_task<kWideG>(ch, a.H, t)) return;
+  const int dh = a.dh;
+  const long ph = (long)dh * dh + dh;
+  const WideSlice<NB> w{t.q, dh};
+  const int sb = ch.x;
+  const long off_b = a.off[sb];
+  const long Nb = a.off[sb + 1] - off_b;
+  const float inv_nsrc = 1.0f / (float)a.nsrc;
+  const float* qrow = a.q + t.n * a.ldq + (long)t.h * dh;
+  float qs[NB][4], dO[NB][4], dq[NB][4];
+  wide_load(qs, qrow, w);
+  if (a.dhr == 0) {
+    wide_load(dO, a.dres + off_b * (long)a.H * dh + ((long)t.h * Nb + (t.n - off_b)) * dh, w);
+  } else {
+    const float* src = a.dres + off_b * (long)a.H * a.dhr + ((long)t.h * Nb + (t.n - off_b)) * a.dhr;
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) dO[b][c] = w.f(b) + c < a.dhr ? src[w.f(b) + c] : 0.f;
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      dq[b][c] = dO[b][c];
+      dO[b][c] *= inv_nsrc;
+    }
+  for (int s = 0; s < a.nsrc; ++s) {
+    const float* S = a.state[s] + (long)sb * a.H * ph + t.h * ph;
+    float zs[NB][4], u[NB][4], pr[NB][4];
+    wide_load(zs, S + (long)dh * dh, w);
+    const float den = group_sum<kWideG>(wide_dot(qs, zs));
+    wide_zero(u);
+#pragma unroll
+    for (int kb = 0; kb < NB; ++kb) wide_rows(S, qrow, dO, kb, w, u, pr[kb]);
+    const float dot = group_sum<kWideG>(wide_dot(dO, u));
+    const float inv = 1.0f / den;
+    const float dden = -dot * inv * inv;
+    float du[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) du[b][c] = dO[b][c] * inv;
+    wide_store(a.du[s] + t.n * a.lddu + (long)t.h * dh, du, w);
+    if (t.q == 0) a.dden[s][t.n * a.H + t.h] = dden;
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) dq[b][c] = fmaf(pr[b][c], inv, fmaf(dden, zs[b][c], dq[b][c]));
+  }
+  const float qdq = group_sum<kWideG>(wide_dot(qs, dq));
+  float dpre[NB][4];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) dpre[b][c] = qs[b][c] * (dq[b][c] - qdq);
+  wide_store(a.dq_pre + t.n * a.lddq + (long)t.h * dh, dpre, w);
+}
+
+template <int NB>
+GNOT_DEV void attn_kv_bwd_wide_body(const AttnKVBwdArgs& a, const int4& ch) {
+  Task t;
+  if (!decode_task<kWideG>(ch, a.H, t)) return;
+  const int dh = a.dh;
+  const long ph = (long)dh * dh + dh;
+  const WideSlice<NB> w{t.q, dh};
+  const float* dS = a.dstate + (long)ch.x * a.H * ph + t.h * ph;
+  const float* krow = a.k + t.n * a.ldkv + (long)t.h * dh;
+  float ks[NB][4], vs[NB][4], dv[NB][4], pr[NB][4], dk[NB][4];
+  wide_load(ks, krow, w);
+  wide_load(vs, a.v + t.n * a.ldkv + (long)t.h * dh, w);
+  wide_zero(dv);
+#pragma unroll
+  for (int kb = 0; kb < NB; ++kb) wide_rows(dS, krow, vs, kb, w, dv, pr[kb]);
+  wide_load(dk, dS + (long)dh * dh, w);
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) dk[b][c] += pr[b][c];
+  const float kdk = group_sum<kWideG>(wide_dot(ks, dk));
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) dk[b][c] = ks[b][c] * (dk[b][c] - kdk);
+  wide_store(a.dk + t.n * a.lddkv + (long)t.h * dh, dk, w);
+  wide_store(a.dv + t.n * a.lddkv + (long)t.h * dh, dv, w);
+}
+
+template <int NB>
+__global__ void __launch_bounds__(256) attn_kv_bwd_wide_kernel(AttnKVBwdArgs a) {
+  attn_kv_bwd_wide_body<NB>(a, a.chunks[blockIdx.x]);
+}
+
+template <int NB>
+__global__ void __launch_bounds__(256) attn_kv_bwd_wide_batch_kernel(const AttnKVBwdArgs* __restrict__ jobs) {
+  const AttnKVBwdArgs& a = jobs[blockIdx.z];
+  if ((int)blockIdx.x >= a.nchunks) return;
+  attn_kv_bwd_wide_body<NB>(a, a.chunks[blockIdx.x]);
+}
+
+// workgroups per 64-point segment of the wide forms: 64 H groups of 16 lanes
+static unsigned wide_split(int H) { return (unsigned)((64 * H * kWideG + 255) / 256); }
+
+#define GNOT_WIDE_SWITCH(DHV, ...)                                            \
+  switch ((DHV + 63) / 64) {                                                  \
+    case 2: { constexpr int NB = 2; __VA_ARGS__; } break;                     \
+    case 3: { constexpr int NB = 3; __VA_ARGS__; } break;                     \
+    case 4: { constexpr int NB = 4; __VA_ARGS__; } break;                     \
+    default: return hipErrorInvalidValue;                                     \
+  }
+
 #define GNOT_DH_SWITCH(DHV, ...)        \
   switch (DHV) {                        \
     case 4: { constexpr int DH = 4; __VA_ARGS__; } break;    \
@@ -345,6 +606,12 @@ hipError_t launch_attn_apply_fwd(const AttnApplyArgs& a, hipStream_t s) {
   if (a.nchunks <= 0) return hipSuccess;
   const hipError_t m = launch_attn_apply_mfma(a, false, s);   // attn_mfma.hip where it applies
   if (m != hipErrorNotSupported) return m;
+  if (a.dh > 64) {
+    if (a.dh % 4 != 0) return hipErrorInvalidValue;
+    GNOT_WIDE_SWITCH(a.dh, hipLaunchKernelGGL(attn_apply_fwd_wide_kernel<NB>, dim3(a.nchunks, wide_split(a.H)),
+                                              dim3(256), 0, s, a));
+    return hipGetLastError();
+  }
   GNOT_DH_SWITCH(a.dh, hipLaunchKernelGGL(attn_apply_fwd_kernel<DH>, dim3(a.nchunks, seg_split<DH>(a.H)), dim3(256),
                                           0, s, a));
   return hipGetLastError();
@@ -354,6 +621,12 @@ hipError_t launch_attn_apply_bwd(const AttnApplyArgs& a, hipStream_t s) {
   if (a.nchunks <= 0) return hipSuccess;
   const hipError_t m = launch_attn_apply_mfma(a, true, s);
   if (m != hipErrorNotSupported) return m;
+  if (a.dh > 64) {
+    if (a.dh % 4 != 0) return hipErrorInvalidValue;
+    GNOT_WIDE_SWITCH(a.dh, hipLaunchKernelGGL(attn_apply_bwd_wide_kernel<NB>, dim3(a.nchunks, wide_split(a.H)),
+                                              dim3(256), 0, s, a));
+    return hipGetLastError();
+  }
   GNOT_DH_SWITCH(a.dh, hipLaunchKernelGGL(attn_apply_bwd_kernel<DH>, dim3(a.nchunks, seg_split<DH>(a.H)), dim3(256),
                                           0, s, a));
   return hipGetLastError();
@@ -363,6 +636,12 @@ hipError_t launch_attn_kv_bwd(const AttnKVBwdArgs& a, hipStream_t s) {
   if (a.nchunks <= 0) return hipSuccess;
   const hipError_t m = launch_attn_kv_bwd_mfma(&a, nullptr, 1, a.nchunks, a.H, a.dh, s);
   if (m != hipErrorNotSupported) return m;
+  if (a.dh > 64) {
+    if (a.dh % 4 != 0) return hipErrorInvalidValue;
+    GNOT_WIDE_SWITCH(a.dh, hipLaunchKernelGGL(attn_kv_bwd_wide_kernel<NB>, dim3(a.nchunks, wide_split(a.H)),
+                                              dim3(256), 0, s, a));
+    return hipGetLastError();
+  }
   GNOT_DH_SWITCH(a.dh, hipLaunchKernelGGL(attn_kv_bwd_kernel<DH>, dim3(a.nchunks, seg_split<DH>(a.H)), dim3(256), 0,
                                           s, a));
   return hipGetLastError();
@@ -374,6 +653,12 @@ hipError_t launch_attn_kv_bwd_batch(const AttnKVBwdArgs* jobs_dev, int njobs, in
   // the batched jobs' pitches are 4-aligned by construction (rows of d floats)
   const hipError_t m = launch_attn_kv_bwd_mfma(nullptr, jobs_dev, njobs, maxchunks, H, dh, s);
   if (m != hipErrorNotSupported) return m;
+  if (dh > 64) {
+    if (dh % 4 != 0) return hipErrorInvalidValue;
+    GNOT_WIDE_SWITCH(dh, hipLaunchKernelGGL(attn_kv_bwd_wide_batch_kernel<NB>, dim3(maxchunks, wide_split(H), njobs),
+                                            dim3(256), 0, s, jobs_dev));
+    return hipGetLastError();
+  }
   GNOT_DH_SWITCH(dh, hipLaunchKernelGGL(attn_kv_bwd_batch_kernel<DH>, dim3(maxchunks, seg_split<DH>(H), njobs),
                                         dim3(256), 0, s, jobs_dev));
   return hipGetLastError();

@@ -328,7 +328,8 @@ extern "C" int gnot_plan_create(const gnot_config* cfg, gnot_plan** out) {
   const int dh = (dhr + 3) / 4 * 4;
   // chain.hip / linear.hip run any multiple of 16 up to 192 (whole 16-wide MFMA tiles, activations in
   // registers), chain2.hip / linear2.hip d = 256; the attention passes any head width that is a multiple
-  // of 4 up to 64 (4-aligned lane slices, attn.hip; the fp32-MFMA forms at 16 / 32 / 64).  A width below
+  // of 4 up to 256 (4-aligned lane slices up to 64, quads over 16 lanes above, attn.hip; the fp32-MFMA forms
+  // at 16 / 32 / 64).  A width below
   // 192 that is not a multiple of 16 runs padded to the next multiple, one in (192, 256) padded to 256
   // (Dr real columns + zero pads); padded heads need H * dh columns
   int D = Dr;
@@ -345,13 +346,16 @@ extern "C" int gnot_plan_create(const gnot_config* cfg, gnot_plan** out) {
     return fail(GNOT_E_INVALID, "hidden width must be at most 512 on the MI355X kernels");
   if (D > 256 && 64 % dh != 0)
     return fail(GNOT_E_INVALID, "above hidden width 256 the head width must divide 64 on the MI355X kernels");
-  if (dh % 4 != 0 || dh > 64)
-    return fail(GNOT_E_INVALID, "head width d/n_head must be a multiple of 4 up to 64 on the MI355X kernels");
+  // attn.hip: 4-aligned lane slices of a head up to 64 features, the wide forms (16 lanes per head, quads
+  // round-robin) above, up to 256
+  if (dh % 4 != 0 || dh > 256)
+    return fail(GNOT_E_INVALID, "head width d/n_head must be a multiple of 4 up to 256 on the MI355X kernels");
   // the projections' fused feature softmax needs whole heads per workgroup: linear2.hip (d = 256) takes
-  // dh = 16 / 32 / 64; linear.hip (the d <= 192 projections and the batched input-function K/V at any d)
-  // a tiling of whole heads (linear_oc)
-  if (D == 256 && dh != 16 && dh != 32 && dh != 64)
-    return fail(GNOT_E_INVALID, "above hidden width 192 the head width must be 16, 32 or 64 on the MI355X kernels");
+  // dh = 16 / 32 / 64 / 128 / 256; linear.hip (the d <= 192 projections and the batched input-function K/V at
+  // any d) a tiling of whole heads (linear_oc)
+  if (D == 256 && dh != 16 && dh != 32 && dh != 64 && dh != 128 && dh != 256)
+    return fail(GNOT_E_INVALID, "above hidden width 192 the head width must be 16, 32, 64, 128 or 256 on the MI355X "
+                                "kernels");
   if ((D != 256 && (linear_oc(D, 3 * D, 2 * D, dh) < 0 || linear_oc(D, D, D, dh) < 0)) || linear_oc(D, 2 * D, 1, dh) < 0)
     return fail(GNOT_E_INVALID, "no projection tiling keeps whole heads of this head width on the MI355X kernels");
   if (c.n_expert < 1 || c.n_attn_layers < 0 || c.n_input_functions < 0 || c.n_input_functions > 8)

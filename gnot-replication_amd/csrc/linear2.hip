@@ -48,29 +48,37 @@ __global__ void __launch_bounds__(64 * l2_waves<NP>(), 2) linear2_kernel(LinearA
     c2_split<DT, NP>(x, bp);
   }
   // bias of the next head group and the old output rows (EPI_ACCUM) are loaded one group ahead / before
-  // the MFMAs: a load placed after a barrier would expose its full latency on every tile
-  float4 bn[TPH];
+  // the MFMAs: a load placed after a barrier would expose its full latency on every tile.  Heads of 128 / 256
+  // features (TPH 8 / 16) load them at their use instead (three TPH-float4 arrays would not fit beside h)
+  constexpr bool PF = TPH <= 4;
+  constexpr int NPF = PF ? TPH : 1;
+  const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 bn[NPF];
+  if constexpr (PF) {
 #pragma unroll
-  for (int k = 0; k < TPH; ++k) bn[k] = a.bias ? ld4(a.bias + 16 * (ob + k) + 4 * g) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < TPH; ++k) bn[k] = a.bias ? ld4(a.bias + 16 * (ob + k) + 4 * g) : zero4;
+  }
   const long pc = valid ? p : 0;
   for (int o0 = ob; o0 < oe; o0 += TPH) {
     float h[TPH][4];
-    float4 bc[TPH], old[TPH];
+    float4 bc[NPF], old[NPF];
+    if constexpr (PF) {
 #pragma unroll
-    for (int k = 0; k < TPH; ++k) {
-      bc[k] = bn[k];
-      if (a.bias && o0 + TPH < oe) bn[k] = ld4(a.bias + 16 * (o0 + TPH + k) + 4 * g);
-      if (a.epi == EPI_ACCUM && !(a.ncol > 0 && 16 * (o0 + k) + 4 * g >= a.ncol))
-        old[k] = ld4(a.Y + pc * a.ldy + 16 * (o0 + k) + 4 * g);
+      for (int k = 0; k < TPH; ++k) {
+        bc[k] = bn[k];
+        if (a.bias && o0 + TPH < oe) bn[k] = ld4(a.bias + 16 * (o0 + TPH + k) + 4 * g);
+        if (a.epi == EPI_ACCUM && !(a.ncol > 0 && 16 * (o0 + k) + 4 * g >= a.ncol))
+          old[k] = ld4(a.Y + pc * a.ldy + 16 * (o0 + k) + 4 * g);
+      }
     }
 #pragma unroll
     for (int k = 0; k < TPH; ++k) {
       const int o = o0 + k;
       const u32x4* cb = st.begin(W, o, oe, c2_tile_u4(KB, NP), nullptr, 0);
+      const float4 b0 = PF ? bc[PF ? k : 0] : (a.bias ? ld4(a.bias + 16 * o + 4 * g) : zero4);
       // the epilogue form with no epilogue: its scheduling fences keep k-block t+1's fragment reads ahead
       // of block t's MFMAs (the plain form compiled to reads issued next to their MFMAs here)
-      const f32x4 acc = c2_tile_epi<KB, NP, true>(cb, bp, f32x4{bc[k].x, bc[k].y, bc[k].z, bc[k].w}, lane,
-                                                  [](int) {});
+      const f32x4 acc = c2_tile_epi<KB, NP, true>(cb, bp, f32x4{b0.x, b0.y, b0.z, b0.w}, lane, [](int) {});
 #pragma unroll
       for (int r = 0; r < 4; ++r) h[k][r] = acc[r];
     }
@@ -107,7 +115,10 @@ __global__ void __launch_bounds__(64 * l2_waves<NP>(), 2) linear2_kernel(LinearA
         const int f = 16 * (o0 + k) + 4 * g;
         if (a.ncol > 0 && f >= a.ncol) continue;     // a row pitch below NO (ncol a multiple of 4)
         float4 v = make_float4(h[k][0], h[k][1], h[k][2], h[k][3]);
-        if (a.epi == EPI_ACCUM) { v.x += old[k].x; v.y += old[k].y; v.z += old[k].z; v.w += old[k].w; }
+        if (a.epi == EPI_ACCUM) {
+          const float4 ov = PF ? old[PF ? k : 0] : ld4(a.Y + p * a.ldy + f);
+          v.x += ov.x; v.y += ov.y; v.z += ov.z; v.w += ov.w;
+        }
         *reinterpret_cast<float4*>(a.Y + p * a.ldy + f) = v;
       }
     }
@@ -173,7 +184,8 @@ bool linear2_supported(const LinearArgs& a, int D) {
   // K < 256: the input rows are read zero-filled past K (a padded width's scramble rows)
   return D == 256 && a.K >= 1 && a.K <= 256 && a.nsum == 1 && a.NO % 16 == 0 && (a.ldx & 3) == 0 &&
          (a.ldy & 3) == 0 && (a.ncol & 3) == 0 && (a.dreal & 15) == 0 &&
-         (a.nseg == 1 ? (a.nsoft == 0 || a.dh == 16 || a.dh == 32 || a.dh == 64) : (a.NO == 256 && a.nsoft == 0 && a.ncol == 0));
+         (a.nseg == 1 ? (a.nsoft == 0 || a.dh == 16 || a.dh == 32 || a.dh == 64 || a.dh == 128 || a.dh == 256)
+                      : (a.NO == 256 && a.nsoft == 0 && a.ncol == 0));
 }
 
 // output-tile chunks per launch: enough workgroups for two per CU (their register budget) on small batches
@@ -199,7 +211,8 @@ static hipError_t launch_linear2_np(const LinearArgs& a, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
     for (const void* f : {reinterpret_cast<const void*>(linear2_kernel<1, NP>), reinterpret_cast<const void*>(linear2_kernel<2, NP>),
-                          reinterpret_cast<const void*>(linear2_kernel<4, NP>), reinterpret_cast<const void*>(linear2_seg_kernel<NP>)})
+                          reinterpret_cast<const void*>(linear2_kernel<4, NP>), reinterpret_cast<const void*>(linear2_kernel<8, NP>),
+                          reinterpret_cast<const void*>(linear2_kernel<16, NP>), reinterpret_cast<const void*>(linear2_seg_kernel<NP>)})
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
@@ -208,7 +221,9 @@ static hipError_t launch_linear2_np(const LinearArgs& a, hipStream_t s) {
   } else {
     if (tph == 1) hipLaunchKernelGGL((linear2_kernel<1, NP>), grid, block, lds, s, a);
     else if (tph == 2) hipLaunchKernelGGL((linear2_kernel<2, NP>), grid, block, lds, s, a);
-    else hipLaunchKernelGGL((linear2_kernel<4, NP>), grid, block, lds, s, a);
+    else if (tph == 4) hipLaunchKernelGGL((linear2_kernel<4, NP>), grid, block, lds, s, a);
+    else if (tph == 8) hipLaunchKernelGGL((linear2_kernel<8, NP>), grid, block, lds, s, a);
+    else hipLaunchKernelGGL((linear2_kernel<16, NP>), grid, block, lds, s, a);
   }
   return hipGetLastError();
 }

@@ -34,8 +34,9 @@ typedef struct gnot_plan gnot_plan; /* opaque */
  * n_attn_hidden_dim, n_mlp_hidden_dim and n_input_hidden_dim must be equal (the reference's
  * residual adds, model.py:131/137, require it); d up to 512 (a d that is not a multiple of 16 up to 192, 256,
  * or a multiple of 64 above it runs on the next of those widths with exact-zero pad columns; parameters,
- * gradients and outputs keep d); d/n_head up to 64 (one that is not a multiple of 4 runs on heads padded to
- * one while n_head times that stays <= 192), 16 / 32 / 64 in (192, 256], and a divisor of 64 above 256. */
+ * gradients and outputs keep d); d/n_head up to 256 (one that is not a multiple of 4 runs on heads padded to
+ * one while n_head times that stays <= 192), 16 / 32 / 64 / 128 / 256 in (192, 256], and a divisor of 64
+ * above 256. */
 typedef struct gnot_config {
   int input_dim;
   int theta_dim;

@@ -2,7 +2,8 @@
 n_head (model.py:41).  This core takes every hidden width d up to 192 (the chain.hip / linear.hip
 kernels, whole 16-wide MFMA tiles; a d that is not a multiple of 16 runs padded to the next one with
 exact-zero pad columns) and d = 256 (chain2.hip / linear2.hip; d in (192, 256) padded to it), with
-any head width dh = d / H up to 64 (the attention passes split a head into 4-aligned lane slices; the
+any head width dh = d / H up to 256 (the attention passes split a head into 4-aligned lane slices up to 64,
+into 4-feature quads dealt round-robin over 16 lanes above; the
 projections' feature softmax reduces a head that straddles 16-feature tiles across the 4 lane groups of a
 point, gnot_common.h softmax_heads; a head width that is not a multiple of 4 runs on heads padded to one,
 up to an internal width of 192).
@@ -61,6 +62,15 @@ CASES = {
     # now loops over any number of its 4 x 4 blocks per thread); H = 8 also runs the MFMA state kernel
     "d320_h5": _cfg(320, 5, 2, 1),
     "d512_h8": _cfg(512, 8, 2, 1),
+    # heads wider than 64 (round 6): attn.hip's wide forms (16 lanes per head, 4-feature quads round-robin,
+    # the q / k row read through the L1), linear2.hip's 128- and 256-feature softmax heads at d = 256
+    "d128_h1": _cfg(128, 1, 2, 1),        # dh 128: one head (two 64-feature blocks)
+    "d256_h2": _cfg(256, 2, 2, 1),        # dh 128 on the d = 256 kernels
+    "d256_h1": _cfg(256, 1, 3, 1, nl=2),  # dh 256 (four blocks; batched input-function K / V at oc 16)
+    "d192_h2": _cfg(192, 2, 2, 0),        # dh 96: a half-filled second block, self-attention only
+    "d136_h2": _cfg(136, 2, 2, 2),        # dh 68 (one quad in block 1), kernels at d = 144, two input functions
+    "d150_h1": _cfg(150, 1, 2, 1),        # dh 150 -> 152: a padded wide head, kernels at d = 160
+    "d184_h2": _cfg(184, 2, 2, 1),        # dh 92 at a padded width (kernels at d = 192)
 }
 
 
