@@ -323,39 +323,26 @@ extern "C" int gnot_plan_create(const gnot_config* cfg, gnot_plan** out) {
   if (c.n_head <= 0 || Dr <= 0 || Dr % c.n_head != 0)
     return fail(GNOT_E_INVALID, "n_embed should be divisible by head");   // model.py:41
   const int dhr = Dr / c.n_head;
-  // the attention passes take head widths that are a multiple of 4 (4-aligned lane slices, attn.hip); any
-  // other runs on heads padded to the next multiple of 4 (gnot_plan::head_padded), at d <= 192
+  // the attention passes take head widths that are a multiple of 4 (4-aligned lane slices up to 64, 4-feature
+  // quads over 16 lanes above, attn.hip; the fp32-MFMA forms at 16 / 32 / 64); any other runs on heads padded
+  // to the next multiple of 4 (gnot_plan::head_padded): q / k / v rows at h * dh, H * dh internal columns
   const int dh = (dhr + 3) / 4 * 4;
-  // chain.hip / linear.hip run any multiple of 16 up to 192 (whole 16-wide MFMA tiles, activations in
-  // registers), chain2.hip / linear2.hip d = 256; the attention passes any head width that is a multiple
-  // of 4 up to 256 (4-aligned lane slices up to 64, quads over 16 lanes above, attn.hip; the fp32-MFMA forms
-  // at 16 / 32 / 64).  A width below
-  // 192 that is not a multiple of 16 runs padded to the next multiple, one in (192, 256) padded to 256
-  // (Dr real columns + zero pads); padded heads need H * dh columns
-  int D = Dr;
-  if (Dr % 16 != 0 && Dr < 192) D = (Dr + 15) / 16 * 16;
-  else if (Dr > 192 && Dr < 256) D = 256;            // chain2.hip / linear2.hip with pad columns
-  else if (Dr > 256) D = (Dr + 63) / 64 * 64;         // 320 .. 512: chainw.hip (one Linear at a time)
-  if (dh != dhr) {
-    D = std::max(D, (c.n_head * dh + 15) / 16 * 16);
-    if (D > 192)
-      return fail(GNOT_E_INVALID, "a head width d/n_head that is not a multiple of 4 runs (on heads padded to "
-                                  "one) up to an internal width of 192 on the MI355X kernels");
-  }
-  if (!((D % 16 == 0 && D >= 16 && D <= 192) || D == 256 || (D > 256 && D <= 512)))
-    return fail(GNOT_E_INVALID, "hidden width must be at most 512 on the MI355X kernels");
-  if (D > 256 && 64 % dh != 0)
-    return fail(GNOT_E_INVALID, "above hidden width 256 the head width must divide 64 on the MI355X kernels");
-  // attn.hip: 4-aligned lane slices of a head up to 64 features, the wide forms (16 lanes per head, quads
-  // round-robin) above, up to 256
-  if (dh % 4 != 0 || dh > 256)
-    return fail(GNOT_E_INVALID, "head width d/n_head must be a multiple of 4 up to 256 on the MI355X kernels");
-  // the projections' fused feature softmax needs whole heads per workgroup: linear2.hip (d = 256) takes
-  // dh = 16 / 32 / 64 / 128 / 256; linear.hip (the d <= 192 projections and the batched input-function K/V at
-  // any d) a tiling of whole heads (linear_oc)
-  if (D == 256 && dh != 16 && dh != 32 && dh != 64 && dh != 128 && dh != 256)
-    return fail(GNOT_E_INVALID, "above hidden width 192 the head width must be 16, 32, 64, 128 or 256 on the MI355X "
-                                "kernels");
+  if (dh > 256)
+    return fail(GNOT_E_INVALID, "head width d/n_head must be at most 256 on the MI355X kernels");
+  // the internal width D (Dr real columns + exact-zero pad columns): chain.hip / linear.hip run any multiple of
+  // 16 up to 192 (whole 16-wide MFMA tiles, activations in registers); chain2.hip / linear2.hip d = 256 with
+  // unpadded heads of 16 / 32 / 64 / 128 / 256 (the projections' softmax head groups); everything else up to
+  // 512 runs at the next multiple of 64 from 320 on chainw.hip (one Linear at a time on linear.hip, whose
+  // whole-row tilings keep any head in one workgroup)
+  const int need = std::max(Dr, c.n_head * dh);
+  const bool l2_heads = dh == dhr && (dh == 16 || dh == 32 || dh == 64 || dh == 128 || dh == 256);
+  int D;
+  if (need <= 192) D = (need + 15) / 16 * 16;
+  else if (need <= 256 && l2_heads) D = 256;
+  else D = std::max(320, (need + 63) / 64 * 64);
+  if (D > 512)
+    return fail(GNOT_E_INVALID, "hidden width must be at most 512 on the MI355X kernels (n_head times the head "
+                                "width rounded up to a multiple of 4, with padded heads)");
   if ((D != 256 && (linear_oc(D, 3 * D, 2 * D, dh) < 0 || linear_oc(D, D, D, dh) < 0)) || linear_oc(D, 2 * D, 1, dh) < 0)
     return fail(GNOT_E_INVALID, "no projection tiling keeps whole heads of this head width on the MI355X kernels");
   if (c.n_expert < 1 || c.n_attn_layers < 0 || c.n_input_functions < 0 || c.n_input_functions > 8)

@@ -203,8 +203,9 @@ int linear_oc(int D, int NO, int nsoft, int dh) {
   return -1;
 }
 
-// every (D, oc) linear_oc can return: oc a divisor of D / 16 (<= 8, or D / 16 itself; at d = 256 the batched
-// input-function K / V with one head of 256 take the whole row)
+// every (D, oc) linear_oc can return: oc a divisor of D / 16 (<= 8, or D / 16 itself: the whole row, which
+// keeps any head in one workgroup -- d = 256's batched input-function K / V with one head of 256, the d > 256
+// projections with heads that do not divide 64)
 #define GNOT_LIN_CASES                                                                                  \
   GNOT_LIN(16, 1) GNOT_LIN(32, 1) GNOT_LIN(32, 2) GNOT_LIN(48, 1) GNOT_LIN(48, 3) GNOT_LIN(64, 1)         \
   GNOT_LIN(64, 2) GNOT_LIN(64, 4) GNOT_LIN(80, 1) GNOT_LIN(80, 5) GNOT_LIN(96, 1) GNOT_LIN(96, 2)         \
@@ -214,7 +215,8 @@ int linear_oc(int D, int NO, int nsoft, int dh) {
   GNOT_LIN(192, 2) GNOT_LIN(192, 3) GNOT_LIN(192, 4) GNOT_LIN(192, 6) GNOT_LIN(192, 12) GNOT_LIN(256, 1)  \
   GNOT_LIN(256, 2) GNOT_LIN(256, 4) GNOT_LIN(256, 8) GNOT_LIN(256, 16) GNOT_LIN(320, 1) GNOT_LIN(320, 2) GNOT_LIN(320, 4)   \
   GNOT_LIN(384, 1) GNOT_LIN(384, 2) GNOT_LIN(384, 4) GNOT_LIN(448, 1) GNOT_LIN(448, 2) GNOT_LIN(448, 4)   \
-  GNOT_LIN(512, 1) GNOT_LIN(512, 2) GNOT_LIN(512, 4)
+  GNOT_LIN(512, 1) GNOT_LIN(512, 2) GNOT_LIN(512, 4) GNOT_LIN(320, 20) GNOT_LIN(384, 24) GNOT_LIN(448, 28) \
+  GNOT_LIN(512, 32)
 // the d <= 192 cases of GNOT_LIN_CASES (the bf16 mode's one-piece kernels)
 #define GNOT_LIN_B1_CASES                                                                                         \
   GNOT_LIN_B1(16, 1) GNOT_LIN_B1(32, 1) GNOT_LIN_B1(32, 2) GNOT_LIN_B1(48, 1) GNOT_LIN_B1(48, 3) GNOT_LIN_B1(64, 1)   \

@@ -32,11 +32,11 @@ typedef struct gnot_plan gnot_plan; /* opaque */
 
 /* GNOT constructor arguments, reference model.py:143 (positional order of main.py:44).
  * n_attn_hidden_dim, n_mlp_hidden_dim and n_input_hidden_dim must be equal (the reference's
- * residual adds, model.py:131/137, require it); d up to 512 (a d that is not a multiple of 16 up to 192, 256,
- * or a multiple of 64 above it runs on the next of those widths with exact-zero pad columns; parameters,
- * gradients and outputs keep d); d/n_head up to 256 (one that is not a multiple of 4 runs on heads padded to
- * one while n_head times that stays <= 192), 16 / 32 / 64 / 128 / 256 in (192, 256], and a divisor of 64
- * above 256. */
+ * residual adds, model.py:131/137, require it); any d and n_head with d/n_head up to 256 whose internal width
+ * is at most 512: a head width that is not a multiple of 4 runs on heads padded to one (n_head x that many
+ * internal columns), and the internal width is the next multiple of 16 up to 192, 256 (heads of 16 / 32 / 64 /
+ * 128 / 256, unpadded), else the next multiple of 64 from 320, with exact-zero pad columns; parameters,
+ * gradients and outputs keep d. */
 typedef struct gnot_config {
   int input_dim;
   int theta_dim;

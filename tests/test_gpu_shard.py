@@ -128,6 +128,10 @@ def test_point_sharded_gnot_matches_oracle(world, case):
     (2, dict(cfg=dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=2, n_attn_layers=1, d=100,
                       n_mlp_num_layers=2, n_expert=2, n_head=4, n_input_functions=1),
              Ns=[121, 66], Ms=[[33, 20]])),
+    # heads of 25 padded to 28 past an internal 192: kernels at 320 (one Linear at a time)
+    (2, dict(cfg=dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=1, d=250,
+                      n_mlp_num_layers=2, n_expert=2, n_head=10, n_input_functions=1),
+             Ns=[90, 61], Ms=[[30, 22]])),
     # one head of 128 (attn.hip's wide forms; the state all-reduce and scramble exchange at dh = 128)
     (2, dict(cfg=dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=1, d=128,
                       n_mlp_num_layers=2, n_expert=2, n_head=1, n_input_functions=1),

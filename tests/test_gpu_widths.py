@@ -1,12 +1,13 @@
 """Hidden and head widths beyond the BASELINE configs: the reference accepts any n_embed divisible by
-n_head (model.py:41).  This core takes every hidden width d up to 192 (the chain.hip / linear.hip
-kernels, whole 16-wide MFMA tiles; a d that is not a multiple of 16 runs padded to the next one with
-exact-zero pad columns) and d = 256 (chain2.hip / linear2.hip; d in (192, 256) padded to it), with
-any head width dh = d / H up to 256 (the attention passes split a head into 4-aligned lane slices up to 64,
-into 4-feature quads dealt round-robin over 16 lanes above; the
-projections' feature softmax reduces a head that straddles 16-feature tiles across the 4 lane groups of a
-point, gnot_common.h softmax_heads; a head width that is not a multiple of 4 runs on heads padded to one,
-up to an internal width of 192).
+n_head (model.py:41).  This core takes every (d, n_head) with a head width up to 256 whose internal width
+is at most 512 (engine.cpp gnot_plan_create): the chain.hip / linear.hip kernels at any multiple of 16 up to
+192 (whole 16-wide MFMA tiles; a d that is not a multiple of 16 runs padded with exact-zero pad columns),
+chain2.hip / linear2.hip at 256 (heads of 16 / 32 / 64 / 128 / 256), and everything else at the next
+multiple of 64 from 320 on the one-Linear-at-a-time chains (chainw.hip, linear.hip's whole-row projection
+tilings).  The attention passes split a head into 4-aligned lane slices up to 64 and into 4-feature quads
+over 16 lanes above; the projections' feature softmax reduces a head that straddles 16-feature tiles
+across the 4 lane groups of a point (gnot_common.h softmax_heads); a head width that is not a multiple of
+4 runs on heads padded to one.
 
 Each case is checked against the float64 oracle (oracle/gnot_oracle.py, pinned to the reference's
 fixtures) at north_star's 1e-4: output and every parameter gradient (golden_util.check_parity), on a
@@ -71,6 +72,13 @@ CASES = {
     "d136_h2": _cfg(136, 2, 2, 2),        # dh 68 (one quad in block 1), kernels at d = 144, two input functions
     "d150_h1": _cfg(150, 1, 2, 1),        # dh 150 -> 152: a padded wide head, kernels at d = 160
     "d184_h2": _cfg(184, 2, 2, 1),        # dh 92 at a padded width (kernels at d = 192)
+    # (round 6) every width the d = 256 kernels cannot take runs at the next multiple of 64 from 320 on the
+    # one-Linear-at-a-time chains, linear.hip's whole-row projection tilings keeping any head in one workgroup
+    "d250_h10": _cfg(250, 10, 2, 1),      # heads of 25 -> 28: 280 internal columns, kernels at d = 320
+    "d200_h5": _cfg(200, 5, 2, 0),        # heads of 40 (no d = 256 softmax group): kernels at d = 320
+    "d256_h32": _cfg(256, 32, 2, 1, nl=2),  # heads of 8 at d = 256: kernels at d = 320
+    "d384_h3": _cfg(384, 3, 2, 1, nl=2),  # heads of 128 above d = 256 (wide attention, whole-row projections)
+    "d300_h5": _cfg(300, 5, 2, 0),        # heads of 60 at a padded 320
 }
 
 

@@ -115,9 +115,10 @@ def test_padded_widths():
     plan accepts it and its canonical Linears keep the model's width (the parameter shapes); d in
     (192, 256) runs on the d = 256 kernels (head widths 16 / 32 / 64 there), d in (256, 512] on the
     one-Linear-at-a-time chains (chainw.hip; head widths dividing 64); a head width that is not a multiple
-    of 4 runs on heads padded to one while the internal width stays <= 192 (d = 100 with 4 heads of 25:
-    kernels at 112; d = 190 with 10 heads of 19 would need 10 x 20 = 200 columns); head widths above 256
-    (above 64 past d = 256; other than 128 / 256 above 64 in (192, 256]) and d > 512 are refused (round 6: d * dh is no longer bounded -- d = 512 / 320 with heads of 64 run).  (Point sharding takes every width the plan takes, tests/test_gpu_shard.py.)"""
+    of 4 runs on heads padded to one (d = 100 with 4 heads of 25: kernels at 112; d = 190 with 10 heads of
+    19: 10 x 20 = 200 columns, kernels at 320); everything the d = 256 kernels cannot take (heads other than
+    16 / 32 / 64 / 128 / 256, padded heads) runs at the next multiple of 64 from 320; head widths above 256
+    and internal widths above 512 are refused (round 6: d * dh is no longer bounded -- d = 512 / 320 with heads of 64 run).  (Point sharding takes every width the plan takes, tests/test_gpu_shard.py.)"""
     from gnot_amd import _lib
     lib = _lib.load()
     base = dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=1, n_mlp_num_layers=2,
@@ -125,12 +126,16 @@ def test_padded_widths():
     plan = ctypes.c_void_p()
     for d, H, ok in ((36, 3, True), (100, 5, True), (60, 15, True), (208, 13, True), (224, 7, True),
                      (320, 10, True), (288, 18, True), (512, 16, True), (512, 8, True),
-                     (100, 4, True), (21, 7, True), (150, 6, True), (190, 10, False),
-                     (200, 5, False), (184, 2, True), (300, 5, False), (576, 9, False),
+                     (100, 4, True), (21, 7, True), (150, 6, True), (190, 10, True),
+                     (200, 5, True), (184, 2, True), (300, 5, True), (576, 9, False),
                      (320, 5, True),                   # heads of 64 above 256 (d * dh up to 32,768)
                      # heads wider than 64 (round 6): up to 256 at d <= 256 (128 / 256 on the d = 256 kernels)
                      (128, 1, True), (136, 2, True), (192, 2, True), (150, 1, True), (256, 2, True), (256, 1, True),
-                     (240, 2, False), (384, 3, False)):
+                     (240, 2, True), (384, 3, True),
+                     # (round 6) widths the d = 256 kernels cannot take run at the next multiple of 64 from 320 on
+                     # the one-Linear-at-a-time chains: heads padded past an internal 192 (250 = 10 x 25 -> 10 x 28),
+                     # d = 256 with heads of 8 (-> 320); refused: d > 512, heads above 256, 10 x 52 = 520 > 512
+                     (250, 10, True), (256, 32, True), (512, 1, False), (300, 1, False), (510, 10, False)):
         cfg = _lib.GnotConfig(**base, n_attn_hidden_dim=d, n_mlp_hidden_dim=d, n_input_hidden_dim=d, n_head=H)
         rc = lib.gnot_plan_create(ctypes.byref(cfg), ctypes.byref(plan))
         assert (rc == 0) == ok, (d, H, rc)
