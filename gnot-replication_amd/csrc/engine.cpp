@@ -336,13 +336,19 @@ extern "C" int gnot_plan_create(const gnot_config* cfg, gnot_plan** out) {
   // whole-row tilings keep any head in one workgroup)
   const int need = std::max(Dr, c.n_head * dh);
   const bool l2_heads = dh == dhr && (dh == 16 || dh == 32 || dh == 64 || dh == 128 || dh == 256);
+  // Above 512 the internal width is the next multiple of 128 up to 1024: the projections then contract in two
+  // halves of 320 .. 512 (launch_linear's K-split, half images PackJob::kh)
   int D;
   if (need <= 192) D = (need + 15) / 16 * 16;
   else if (need <= 256 && l2_heads) D = 256;
-  else D = std::max(320, (need + 63) / 64 * 64);
-  if (D > 512)
-    return fail(GNOT_E_INVALID, "hidden width must be at most 512 on the MI355X kernels (n_head times the head "
+  else if (need <= 512) D = std::max(320, (need + 63) / 64 * 64);
+  else D = (need + 127) / 128 * 128;
+  if (D > 1024)
+    return fail(GNOT_E_INVALID, "hidden width must be at most 1024 on the MI355X kernels (n_head times the head "
                                 "width rounded up to a multiple of 4, with padded heads)");
+  if (D > 512 && 64 % dh != 0)
+    return fail(GNOT_E_INVALID, "above an internal width of 512 the head width must divide 64 on the MI355X "
+                                "kernels");
   if ((D != 256 && (linear_oc(D, 3 * D, 2 * D, dh) < 0 || linear_oc(D, D, D, dh) < 0)) || linear_oc(D, 2 * D, 1, dh) < 0)
     return fail(GNOT_E_INVALID, "no projection tiling keeps whole heads of this head width on the MI355X kernels");
   if (c.n_expert < 1 || c.n_attn_layers < 0 || c.n_input_functions < 0 || c.n_input_functions > 8)
@@ -505,6 +511,8 @@ static void plan_images(gnot_plan* p) {
     }
     J.transposed = tr;
     J.o0 = o0; J.t0 = t0; J.ktot = im.KT; J.otot = im.OT;
+    // internal widths above 512: a full-width contraction packed as two half images (launch_linear's K-split)
+    if (x6 == 0 && p->D > 512 && im.KT == p->DT) J.kh = p->DT / 2;
     J.OTp = OTp; J.KTp = KTp;
     p->pack_jobs.push_back(J);
     p->pack_dst_off4.push_back(im.off4);
@@ -975,6 +983,23 @@ static void build_groups(gnot_plan* p) {
   }
 }
 
+// internal widths above 512: a batched projection job's segments as K-halves (launch_linear's K-split done on
+// the host: the batched kernel reads its jobs from device memory and runs at D / 2)
+static void ksplit_job(const gnot_plan* p, LinearArgs& a) {
+  if (p->D <= 512) return;
+  const int Kh = p->D / 2;
+  const long half4 = (long)(a.NO / 16) * (Kh / 16) * 64;   // the second half image (64 float4 per tile)
+  LinearArgs b = a;
+  b.nseg = 2 * a.nseg;
+  for (int k = 0; k < b.nseg; ++k) {
+    b.X[k] = a.X[k / 2] + (k % 2) * Kh;
+    b.Wp[k] = a.Wp[k / 2] + (k % 2) * half4;
+  }
+  b.K = Kh;
+  b.dblk = p->D;
+  a = b;
+}
+
 // Device job tables of the batched input-function side of cross attention (pointers are null
 // before bind: sizing only).
 static void build_attn_tables(gnot_plan* p) {
@@ -993,6 +1018,7 @@ static void build_attn_tables(gnot_plan* p) {
       a.bias = pbias + A.bkv[i]; a.Y = p->P_(s + "ckv" + si); a.ldy = 2 * D; a.NO = 2 * D; a.P = (int)p->Q[i];
       a.epi = EPI_STORE; a.nsoft = D; a.dh = p->dh; a.dreal = p->attn_dreal();
       a.dhr = p->head_padded() ? p->dhr : 0;
+      ksplit_job(p, a);
       p->fwd_kv_jobs.push_back(a);
     }
   if (!p->training) return;
@@ -1008,13 +1034,15 @@ static void build_attn_tables(gnot_plan* p) {
       kb.dk = dkv; kb.dv = dkv + D; kb.lddkv = 2 * D;
       p->kvbwd_jobs.push_back(kb);
     }
-  // d(fn encoding i) = sum_l dK_{l,i} Wk_{l,i} + dV_{l,i} Wv_{l,i}: 2L K-segments, <= kMaxSeg per launch
+  // d(fn encoding i) = sum_l dK_{l,i} Wk_{l,i} + dV_{l,i} Wv_{l,i}: 2L K-segments, <= kMaxSeg per launch (half
+  // as many above an internal width of 512, each then two K-halves)
   const int nseg = 2 * L;
-  for (int k0 = 0; k0 < nseg; k0 += kMaxSeg) {
+  const int per = D > 512 ? kMaxSeg / 2 : kMaxSeg;
+  for (int k0 = 0; k0 < nseg; k0 += per) {
     std::vector<LinearArgs> launch;
     for (int i = 0; i < I; ++i) {
       LinearArgs a{};
-      a.nseg = std::min(kMaxSeg, nseg - k0);
+      a.nseg = std::min(per, nseg - k0);
       for (int sg = 0; sg < a.nseg; ++sg) {
         const int l = (k0 + sg) / 2, kv = (k0 + sg) % 2;
         a.X[sg] = p->P_(p->dkv_buf(l, i)) + kv * D;
@@ -1022,6 +1050,7 @@ static void build_attn_tables(gnot_plan* p) {
       }
       a.ldx = 2 * D; a.nsum = 1; a.K = D; a.bias = nullptr; a.Y = p->P_("dfn" + std::to_string(i)); a.ldy = D;
       a.NO = D; a.P = (int)p->Q[i]; a.epi = k0 == 0 ? EPI_STORE : EPI_ACCUM; a.nsoft = 0; a.dh = p->dh;
+      ksplit_job(p, a);
       launch.push_back(a);
     }
     p->dfn_jobs.push_back(launch);
@@ -2075,7 +2104,8 @@ static int forward_impl(gnot_plan* p, const float* x, const float* theta, const 
   if (p->I > 0 && p->L > 0) {
     long Qmax = 0;
     for (long q : p->Q) Qmax = std::max(Qmax, q);
-    GNOT_CK(launch_linear_batch(p->d_fwd_kv_jobs, (int)p->fwd_kv_jobs.size(), (int)Qmax, 2 * D, D, p->dh, cf.s));
+    GNOT_CK(launch_linear_batch(p->d_fwd_kv_jobs, (int)p->fwd_kv_jobs.size(), (int)Qmax, 2 * D, D > 512 ? D / 2 : D,
+                                p->dh, cf.s));
     GNOT_RUN(run_state(cf, p->st_fn));
   }
   if (br) {                                // join the input-function branch
@@ -2218,7 +2248,7 @@ static int backward_impl(gnot_plan* p, const float* dout, void* stream) {
     }
     GNOT_CK(launch_attn_kv_bwd_batch(p->d_kvbwd_jobs, (int)p->kvbwd_jobs.size(), maxch, p->H, p->dh, cf.s));
     for (size_t k = 0; k < p->d_dfn_jobs.size(); ++k)
-      GNOT_CK(launch_linear_batch(p->d_dfn_jobs[k], p->I, (int)Qmax, D, D, p->dh, cf.s));
+      GNOT_CK(launch_linear_batch(p->d_dfn_jobs[k], p->I, (int)Qmax, D, D > 512 ? D / 2 : D, p->dh, cf.s));
     GNOT_RUN(run_wgrad_side(cf, p->wg_fnkv, {}));
   }
   if (p->I > 0 && p->L == 0)   // encodings unused by the output: zero gradients

@@ -31,6 +31,10 @@ struct PackJob {
   // out is then H * hp.  Applies to the image rows (forward) or the contraction index (transposed) and to
   // the bias copy.  0: rows map 1:1
   int hr = 0, hp = 0;
+  // internal widths above 512 (fp32 images): the contraction in two halves of kh tiles, each half a whole
+  // image of its own -- tile (o, T) at ((T / kh) * otot + o) * kh + T % kh -- so that a projection runs as two
+  // K-segments of the 320 .. 512-wide kernels (launch_linear).  0: one image, ktot tiles deep
+  int kh = 0;
 };
 // pack tiles of a job: fp32 images have OTp*KTp tiles, x6 images OTp*ceil(KTp/2) blocks
 inline int pack_tiles(const PackJob& J) { return J.x6 ? J.OTp * ((J.KTp + 1) / 2) : J.OTp * J.KTp; }
@@ -68,7 +72,16 @@ struct LinearArgs {
   // excludes (and writes 0 to) the others.  0: every feature of a head is real
   int dhr = 0;
   int ncol = 0;                      // store only output columns [0, ncol) (row pitch ldy < NO); 0 = all NO
+  // the width of the output blocks dreal / dhr repeat in (the internal width); 0 = the kernel's K width D.
+  // Set by launch_linear's K-split, whose kernels run at half the internal width
+  int dblk = 0;
+  int kcols[kMaxSeg] = {};           // per-segment input columns when they differ (K-split); 0 = K
 };
+// D: the K width the kernel is instantiated at (the internal width for the projections, a layer's input
+// tiles x 16 for the chains).  D in (512, 1024] (a multiple of 128): the contraction runs as two K-halves of
+// every segment on the D / 2 kernels -- X[s] + D / 2 for the second half and an image made of two half
+// images (PackJob::kh), the second (NO / 16) x (D / 32) tiles after the first -- in launches of at most
+// kMaxSeg segments (later ones accumulate; a softmax epilogue must fit one launch); a.K must then be D
 hipError_t launch_linear(const LinearArgs& a, int D, hipStream_t s);
 // output tiles per workgroup of linear.hip for an NO-column projection with a softmax epilogue over its
 // first nsoft columns in heads of dh (-1: no tiling keeps whole heads per workgroup)
@@ -184,7 +197,14 @@ hipError_t launch_wgrad_b16(const WgradJob* jobs_dev, const int* wg_prefix_dev, 
 // [H][dh*dh + dh], `splits` partials of state_pts(d) points each at slab + slab_off.
 // Two kernels: state_mfma (fp32 MFMA, rows straight from HBM, dh = 16/32/64 with H % 4 == 0;
 // below GNOT_STATE_MFMA_MIN points the VALU form) and the VALU state_partial (LDS-staged rows, any width).
-inline bool state_mfma_ok(int d, int dh) { return (dh == 16 || dh == 32 || dh == 64) && d % dh == 0 && (d / dh) % 4 == 0; }
+// (the instantiated state_mfma_kernel<DH, HPW> forms, HPW = heads per wave = d / dh / 4: 1 / 2 / 4 at dh 16 and
+// 32, 1 / 2 at 64; any other head count runs the VALU kernel -- round 6: 12 heads of 16 at d = 192 used to pass
+// this test and fail the launch on meshes past GNOT_STATE_MFMA_MIN)
+inline bool state_mfma_ok(int d, int dh) {
+  if (!((dh == 16 || dh == 32 || dh == 64) && d % dh == 0 && (d / dh) % 4 == 0)) return false;
+  const int hpw = d / dh / 4;
+  return hpw == 1 || hpw == 2 || (hpw == 4 && dh <= 32);
+}
 // points per partial-state workgroup: 256 on MFMA (4 waves per SIMD at 262k points, partials ~6 % of
 // the row bytes); VALU: the workgroup's A and B rows fill <= 32 KiB of LDS each (64 at d <= 128,
 // 8192 / d above; measured: 32 and 16 are slower at cfg2)

@@ -10,6 +10,7 @@
 // weight images (backward-data of the q/k/v projections: dX = dQ Wq + dK Wk + dV Wv in one pass).
 // A batched variant runs independent jobs (e.g. the key/value projections of every block and
 // input function) in one launch.
+#include <algorithm>
 #include <cstdlib>
 
 #include "gnot_common.h"
@@ -87,12 +88,13 @@ GNOT_DEV void linear_body(const LinearArgs& a, float4* wlds) {
   int cnt = 0;
   stage_image(wlds, a.Wp[0] + wchunk, cf4, 4, wave, lane);
 
+  auto kcol = [&](int sg) { return a.kcols[sg] > 0 ? a.kcols[sg] : a.K; };
   // segment 0 input (optionally the sum of nsum equally strided buffers)
   float in[KT][4];
-  load_rows<KT>(in, a.X[0], a.ldx, p, valid, a.K, lane);
+  load_rows<KT>(in, a.X[0], a.ldx, p, valid, kcol(0), lane);
   for (int s = 1; s < a.nsum; ++s) {
     float t[KT][4];
-    load_rows<KT>(t, a.X[0] + s * a.sum_stride, a.ldx, p, valid, a.K, lane);
+    load_rows<KT>(t, a.X[0] + s * a.sum_stride, a.ldx, p, valid, kcol(0), lane);
 #pragma unroll
     for (int T = 0; T < KT; ++T)
 #pragma unroll
@@ -106,7 +108,7 @@ GNOT_DEV void linear_body(const LinearArgs& a, float4* wlds) {
     const bool more = sg + 1 < a.nseg;
     float nx[KT][4];
     auto pre = [&]() {
-      if (more) load_rows<KT>(nx, a.X[sg + 1], a.ldx, p, valid, a.K, lane);
+      if (more) load_rows<KT>(nx, a.X[sg + 1], a.ldx, p, valid, kcol(sg + 1), lane);
     };
     if constexpr (B1) {
       u32x4 bp[KB][NP];
@@ -127,6 +129,7 @@ GNOT_DEV void linear_body(const LinearArgs& a, float4* wlds) {
   }
   float h[OC][4];
   acc_to_regs<OC>(acc, h);
+  const int DB = a.dblk > 0 ? a.dblk : D;          // the width of the output blocks (pad columns, heads)
   if (c * 16 * OC < a.nsoft) {
     if (a.dhr > 0) {
       // padded heads: the pad features of every head (j >= dhr) take no part in its softmax (exp -> 0)
@@ -134,7 +137,7 @@ GNOT_DEV void linear_body(const LinearArgs& a, float4* wlds) {
       for (int T = 0; T < OC; ++T)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          if ((c * 16 * OC + 16 * T + 4 * (lane >> 4) + r) % D % a.dh >= a.dhr) h[T][r] = -INFINITY;
+          if ((c * 16 * OC + 16 * T + 4 * (lane >> 4) + r) % DB % a.dh >= a.dhr) h[T][r] = -INFINITY;
     }
     softmax_heads<OC>(h, a.dh, lane >> 4);
   }
@@ -144,7 +147,7 @@ GNOT_DEV void linear_body(const LinearArgs& a, float4* wlds) {
     for (int T = 0; T < OC; ++T)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        if ((c * 16 * OC + 16 * T + 4 * (lane >> 4) + r) % D >= a.dreal) h[T][r] = 0.f;
+        if ((c * 16 * OC + 16 * T + 4 * (lane >> 4) + r) % DB >= a.dreal) h[T][r] = 0.f;
   }
   const int ncols = a.ncol > 0 ? min(16 * OC, a.ncol - c * 16 * OC) : 16 * OC;
   if (ncols <= 0) return;
@@ -227,9 +230,41 @@ int linear_oc(int D, int NO, int nsoft, int dh) {
   GNOT_LIN_B1(176, 1) GNOT_LIN_B1(176, 11) GNOT_LIN_B1(192, 1) GNOT_LIN_B1(192, 2) GNOT_LIN_B1(192, 3)                 \
   GNOT_LIN_B1(192, 4) GNOT_LIN_B1(192, 6) GNOT_LIN_B1(192, 12)
 
+// internal widths above 512: every segment's contraction in two halves on the D / 2 kernels (see gnot_kernels.h)
+static hipError_t launch_linear_ksplit(const LinearArgs& a, int D, hipStream_t s) {
+  const int Kh = D / 2;
+  // a.K <= D / 2 (an input narrower than the internal width, e.g. a chain's first layer): the first halves only;
+  // otherwise the second halves take the K - D / 2 columns past the first (the real width of a padded input)
+  const int halves = a.K <= Kh ? 1 : 2;
+  if (D > 1024 || D % 128 != 0 || a.K > D || a.nsum != 1 || a.NO % 16 != 0) return hipErrorInvalidValue;
+  for (int sg = 0; sg < a.nseg; ++sg)
+    if (a.kcols[sg] > 0) return hipErrorInvalidValue;     // already split
+  const long half4 = (long)(a.NO / 16) * (Kh / 16) * WAVE;   // the second half image, in float4
+  const int nseg2 = halves * a.nseg;
+  if (a.nsoft > 0 && nseg2 > kMaxSeg) return hipErrorInvalidValue;   // a softmax needs the whole sum at once
+  for (int s0 = 0; s0 < nseg2; s0 += kMaxSeg) {
+    LinearArgs b = a;
+    b.nseg = std::min(kMaxSeg, nseg2 - s0);
+    for (int k = 0; k < b.nseg; ++k) {
+      const int sg = (s0 + k) / halves, h = (s0 + k) % halves;
+      b.X[k] = a.X[sg] + h * Kh;
+      b.Wp[k] = a.Wp[sg] + h * half4;
+      b.kcols[k] = h == 0 ? std::min(a.K, Kh) : a.K - Kh;
+    }
+    for (int k = b.nseg; k < kMaxSeg; ++k) b.kcols[k] = 0;
+    b.K = std::min(a.K, Kh);
+    b.dblk = a.dblk > 0 ? a.dblk : D;
+    if (s0 > 0) { b.epi = EPI_ACCUM; b.bias = nullptr; }
+    const hipError_t r = launch_linear(b, Kh, s);
+    if (r != hipSuccess) return r;
+  }
+  return hipSuccess;
+}
+
 hipError_t launch_linear(const LinearArgs& a, int D, hipStream_t s) {
   if (a.P <= 0) return hipSuccess;
   if (a.nseg < 1 || a.nseg > kMaxSeg) return hipErrorInvalidValue;
+  if (D > 512) return launch_linear_ksplit(a, D, s);
   const int oc = linear_oc(D, a.NO, a.nsoft, a.dh);
   const dim3 grid((a.P + 63) / 64, a.NO / (16 * oc)), block(256);
 #define GNOT_LIN(DD, OO) \

@@ -114,7 +114,10 @@ __global__ void __launch_bounds__(64) pack_kernel(const PackJob* __restrict__ jo
       v[r] = (wr >= 0 && col < J.in) ? J.W[(long)wr * J.in + col] : 0.f;
     }
   }
-  J.dst[((long)(J.o0 + o) * J.ktot + J.t0 + T) * WAVE + lane] = make_float4(v[0], v[1], v[2], v[3]);
+  const int Ta = J.t0 + T;
+  const long di = J.kh > 0 ? ((long)(Ta / J.kh) * J.otot + J.o0 + o) * J.kh + Ta % J.kh
+                           : (long)(J.o0 + o) * J.ktot + Ta;
+  J.dst[di * WAVE + lane] = make_float4(v[0], v[1], v[2], v[3]);
   // padded bias copy, done by the job's first tile
   if (J.bias_dst && t == 0) {
     const int nb = 16 * J.OTp;

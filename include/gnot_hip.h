@@ -33,10 +33,10 @@ typedef struct gnot_plan gnot_plan; /* opaque */
 /* GNOT constructor arguments, reference model.py:143 (positional order of main.py:44).
  * n_attn_hidden_dim, n_mlp_hidden_dim and n_input_hidden_dim must be equal (the reference's
  * residual adds, model.py:131/137, require it); any d and n_head with d/n_head up to 256 whose internal width
- * is at most 512: a head width that is not a multiple of 4 runs on heads padded to one (n_head x that many
+ * is at most 1024: a head width that is not a multiple of 4 runs on heads padded to one (n_head x that many
  * internal columns), and the internal width is the next multiple of 16 up to 192, 256 (heads of 16 / 32 / 64 /
- * 128 / 256, unpadded), else the next multiple of 64 from 320, with exact-zero pad columns; parameters,
- * gradients and outputs keep d. */
+ * 128 / 256, unpadded), the next multiple of 64 up to 512, else the next multiple of 128 (heads dividing 64),
+ * with exact-zero pad columns; parameters, gradients and outputs keep d. */
 typedef struct gnot_config {
   int input_dim;
   int theta_dim;

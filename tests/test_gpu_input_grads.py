@@ -9,7 +9,7 @@ gnot_input_grads combines them (dx = d x_in[:, :in] + d x_gate, d theta = per-sa
 Checked against float64 autograd of the stock-torch port (oracle/torch_port.py; its forward and
 parameter gradients are pinned to the reference's fixtures by tests/test_oracle.py, the input
 gradients are torch's autograd of that same op sequence) at north_star's 1e-4, norm-wise, for
-packed and padded calls, d = 64 (chain.hip), d = 256 (chain2.hip), d = 300 (chainw.hip) and d = 100 with
+packed and padded calls, d = 64 (chain.hip), d = 256 (chain2.hip), d = 300 (chainw.hip), d = 576 (K-split projections) and d = 100 with
 heads of 25 (padded heads); and asking for input
 gradients must leave the output and every parameter gradient bitwise unchanged.
 """
@@ -29,6 +29,9 @@ CASES = {
     # d > 256: the chains one Linear at a time (chainw.hip), padded 300 -> 320
     "d300_I1": dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=1, d=300,
                     n_mlp_num_layers=2, n_expert=2, n_head=75, n_input_functions=1),
+    # d > 512: kernels at 640, every full-width contraction in two K-halves
+    "d576_I1": dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=1, d=576,
+                    n_mlp_num_layers=2, n_expert=2, n_head=9, n_input_functions=1),
     # padded heads: 4 heads of 25 run as heads of 28 (the q / k / v images' rows placed per head)
     "d100_h4_I2": dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=2, n_attn_layers=1, d=100,
                        n_mlp_num_layers=2, n_expert=2, n_head=4, n_input_functions=2),
@@ -78,6 +81,7 @@ def _port_grads(cfg, sd64, xs, thetas, fns_per_sample, Gs, autocast=False):
     ("d300_I1", "fp32", False),
     ("d300_I1", "fp32", True),
     ("d100_h4_I2", "fp32", False),
+    ("d576_I1", "fp32", False),
 ])
 def test_input_grads_packed_match_port(name, prec, recompute):
     """north_star's bar per arithmetic: 1e-4 in fp32, 1e-2 in bf16 mode."""

@@ -132,6 +132,10 @@ def test_point_sharded_gnot_matches_oracle(world, case):
     (2, dict(cfg=dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=1, d=250,
                       n_mlp_num_layers=2, n_expert=2, n_head=10, n_input_functions=1),
              Ns=[90, 61], Ms=[[30, 22]])),
+    # d = 576 (kernels at 640: K-split projections; the exchange at the real width)
+    (2, dict(cfg=dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=1, d=576,
+                      n_mlp_num_layers=2, n_expert=2, n_head=9, n_input_functions=1),
+             Ns=[70, 45], Ms=[[25, 18]])),
     # one head of 128 (attn.hip's wide forms; the state all-reduce and scramble exchange at dh = 128)
     (2, dict(cfg=dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=1, d=128,
                       n_mlp_num_layers=2, n_expert=2, n_head=1, n_input_functions=1),

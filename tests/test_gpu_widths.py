@@ -1,10 +1,10 @@
 """Hidden and head widths beyond the BASELINE configs: the reference accepts any n_embed divisible by
 n_head (model.py:41).  This core takes every (d, n_head) with a head width up to 256 whose internal width
-is at most 512 (engine.cpp gnot_plan_create): the chain.hip / linear.hip kernels at any multiple of 16 up to
+is at most 1024 (engine.cpp gnot_plan_create): the chain.hip / linear.hip kernels at any multiple of 16 up to
 192 (whole 16-wide MFMA tiles; a d that is not a multiple of 16 runs padded with exact-zero pad columns),
 chain2.hip / linear2.hip at 256 (heads of 16 / 32 / 64 / 128 / 256), and everything else at the next
 multiple of 64 from 320 on the one-Linear-at-a-time chains (chainw.hip, linear.hip's whole-row projection
-tilings).  The attention passes split a head into 4-aligned lane slices up to 64 and into 4-feature quads
+tilings), above 512 at the next multiple of 128 with every full-width contraction split in two halves.  The attention passes split a head into 4-aligned lane slices up to 64 and into 4-feature quads
 over 16 lanes above; the projections' feature softmax reduces a head that straddles 16-feature tiles
 across the 4 lane groups of a point (gnot_common.h softmax_heads); a head width that is not a multiple of
 4 runs on heads padded to one.
@@ -40,6 +40,7 @@ CASES = {
     "d160_h8": _cfg(160, 8, 2, 1),        # dh 20
     "d192_h8": _cfg(192, 8, 2, 0),        # dh 24, self-attention only
     "d192_h6": _cfg(192, 6, 2, 1, nl=4),  # dh 32 (fp32-MFMA attention forms at d = 192)
+    "d192_h12": _cfg(192, 12, 2, 1),      # dh 16, 12 heads: 3 per wave has no MFMA state form (VALU state)
     # widths that are not a multiple of 16 run padded to the next one (engine.cpp gnot_plan_create: zero pad
     # columns, the feature softmax's pad columns zeroed, the scramble rows at the real width)
     "d36_h3": _cfg(36, 3, 2, 1),          # dh 12, kernels at d = 48
@@ -79,6 +80,12 @@ CASES = {
     "d256_h32": _cfg(256, 32, 2, 1, nl=2),  # heads of 8 at d = 256: kernels at d = 320
     "d384_h3": _cfg(384, 3, 2, 1, nl=2),  # heads of 128 above d = 256 (wide attention, whole-row projections)
     "d300_h5": _cfg(300, 5, 2, 0),        # heads of 60 at a padded 320
+    # (round 6) above 512: the next multiple of 128 up to 1024, every full-width contraction in two halves on the
+    # 320 .. 512 kernels (launch_linear's K-split over half images; the batched input-function K / V and their
+    # backward-data split on the host)
+    "d576_h9": _cfg(576, 9, 2, 1),        # heads of 64, kernels at 640 (fc_out contracts 576 = 320 + 256 columns)
+    "d768_h24": _cfg(768, 24, 2, 0, nl=2),  # heads of 32, self-attention only
+    "d1024_h16": _cfg(1024, 16, 2, 2, nl=2),  # heads of 64, two input functions
 }
 
 

@@ -117,8 +117,8 @@ def test_padded_widths():
     one-Linear-at-a-time chains (chainw.hip; head widths dividing 64); a head width that is not a multiple
     of 4 runs on heads padded to one (d = 100 with 4 heads of 25: kernels at 112; d = 190 with 10 heads of
     19: 10 x 20 = 200 columns, kernels at 320); everything the d = 256 kernels cannot take (heads other than
-    16 / 32 / 64 / 128 / 256, padded heads) runs at the next multiple of 64 from 320; head widths above 256
-    and internal widths above 512 are refused (round 6: d * dh is no longer bounded -- d = 512 / 320 with heads of 64 run).  (Point sharding takes every width the plan takes, tests/test_gpu_shard.py.)"""
+    16 / 32 / 64 / 128 / 256, padded heads) runs at the next multiple of 64 from 320, above 512 at the next
+    multiple of 128 (heads dividing 64); head widths above 256 and internal widths above 1024 are refused (round 6: d * dh is no longer bounded -- d = 512 / 320 with heads of 64 run).  (Point sharding takes every width the plan takes, tests/test_gpu_shard.py.)"""
     from gnot_amd import _lib
     lib = _lib.load()
     base = dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=1, n_mlp_num_layers=2,
@@ -127,7 +127,7 @@ def test_padded_widths():
     for d, H, ok in ((36, 3, True), (100, 5, True), (60, 15, True), (208, 13, True), (224, 7, True),
                      (320, 10, True), (288, 18, True), (512, 16, True), (512, 8, True),
                      (100, 4, True), (21, 7, True), (150, 6, True), (190, 10, True),
-                     (200, 5, True), (184, 2, True), (300, 5, True), (576, 9, False),
+                     (200, 5, True), (184, 2, True), (300, 5, True), (576, 9, True),
                      (320, 5, True),                   # heads of 64 above 256 (d * dh up to 32,768)
                      # heads wider than 64 (round 6): up to 256 at d <= 256 (128 / 256 on the d = 256 kernels)
                      (128, 1, True), (136, 2, True), (192, 2, True), (150, 1, True), (256, 2, True), (256, 1, True),
@@ -135,7 +135,9 @@ def test_padded_widths():
                      # (round 6) widths the d = 256 kernels cannot take run at the next multiple of 64 from 320 on
                      # the one-Linear-at-a-time chains: heads padded past an internal 192 (250 = 10 x 25 -> 10 x 28),
                      # d = 256 with heads of 8 (-> 320); refused: d > 512, heads above 256, 10 x 52 = 520 > 512
-                     (250, 10, True), (256, 32, True), (512, 1, False), (300, 1, False), (510, 10, False)):
+                     (250, 10, True), (256, 32, True), (512, 1, False), (300, 1, False),
+                     # above 512: the next multiple of 128 up to 1024 (K-split projections), heads dividing 64
+                     (510, 10, False), (1024, 16, True), (768, 24, True), (640, 5, False), (1100, 11, False)):
         cfg = _lib.GnotConfig(**base, n_attn_hidden_dim=d, n_mlp_hidden_dim=d, n_input_hidden_dim=d, n_head=H)
         rc = lib.gnot_plan_create(ctypes.byref(cfg), ctypes.byref(plan))
         assert (rc == 0) == ok, (d, H, rc)
