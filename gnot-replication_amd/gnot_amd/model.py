@@ -222,8 +222,9 @@ class GNOT(nn.Module):
         per MFMA in the MLP chains, attention projections and weight gradients of every hidden width up to
         256, fp32 accumulation; at d = 256 the soft-MoE expert chains also keep their training saves
         (gelu'(h), expert outputs), dZ and Linear inputs in bf16, which the MoE weight gradients read
-        directly; parameters, the other activations and the attention contractions stay fp32).  Above
-        d = 256 (the layer-wise chains) the fp32 path runs in either mode."""
+        directly; parameters, the other activations and the attention contractions stay fp32).  Above an
+        internal width of 256 (d > 256, and the head layouts the d = 256 kernels cannot take, e.g. d = 200 with
+        heads of 40: the layer-wise chains) the fp32 path runs in either mode."""
         d = str(dtype).replace("torch.", "")
         if d in ("bf16", "bfloat16"):
             self._bf16 = True
