@@ -182,11 +182,13 @@ def test_width_bf16_mode(name):
     assert rel(out16, out32) > 1e-6
 
 
-def test_bf16_mode_above_256_runs_the_fp32_path():
-    """Above d = 256 (chainw.hip, fp32-MFMA projections) the bf16 mode has no one-piece kernels: the results
+@pytest.mark.parametrize("name", ["d320_h10", "d200_h5", "d576_h9"])
+def test_bf16_mode_above_256_runs_the_fp32_path(name):
+    """Above an internal width of 256 (chainw.hip, fp32-MFMA projections: d > 256, and head layouts the d = 256
+    kernels cannot take, e.g. d = 200 with heads of 40) the bf16 mode has no one-piece kernels: the results
     are the fp32 path's, bit for bit."""
     import numpy as np
-    fx, G = _case("d320_h10")
+    fx, G = _case(name)
     m = build_model(fx["params"], fx["cfg"])
     out32, g32 = run_packed(m, fx, G)
     m.set_precision("bf16")
