@@ -82,6 +82,16 @@ CASES = [
          cfg=dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=1,
                   d=128, n_mlp_num_layers=1, n_expert=4, n_head=8, n_input_functions=2),
          N=[120, 75], M=[[50, 30], [44, 20]]),
+    # round 6: one head of 128 (attn.hip's wide forms: 16 lanes per head, quads round-robin)
+    dict(name="d128_h1_wide", mode="packed", sharp=3.0, fp32_params=True,
+         cfg=dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=1, n_attn_layers=1,
+                  d=128, n_mlp_num_layers=1, n_expert=2, n_head=1, n_input_functions=1),
+         N=[60, 41], M=[[30, 17]]),
+    # padded heads (4 heads of 25, run as heads of 28 at an internal width of 112), padded calling convention
+    dict(name="d100_h4_padheads", mode="padded", sharp=3.0, fp32_params=True,
+         cfg=dict(input_dim=2, theta_dim=1, input_func_dim=3, out_dim=2, n_attn_layers=1,
+                  d=100, n_mlp_num_layers=1, n_expert=2, n_head=4, n_input_functions=1),
+         N=[40, 27], M=[[19, 12]]),
 ]
 
 
