@@ -86,6 +86,7 @@ CASES = {
     "d576_h9": _cfg(576, 9, 2, 1),        # heads of 64, kernels at 640 (fc_out contracts 576 = 320 + 256 columns)
     "d768_h24": _cfg(768, 24, 2, 0, nl=2),  # heads of 32, self-attention only
     "d1024_h16": _cfg(1024, 16, 2, 2, nl=2),  # heads of 64, two input functions
+    "d640_l3": _cfg(640, 10, 2, 1, L=3, nl=1),  # three blocks: the d(fn) backward-data in two accumulating launches
 }
 
 
