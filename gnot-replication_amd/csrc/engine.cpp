@@ -2271,19 +2271,45 @@ static int backward_impl(gnot_plan* p, const float* dout, void* stream) {
     if (p->input_grads) { a.dX = p->P_("dxin"); a.lddx = p->bufs["dxin"].ld; a.dx_chain_stride = 0; }
     GNOT_RUN(chain_bwd(a, p->k_x(), P, p->wg_x, "chain_bwd"));
   }
-  // gating: d scores accumulated over every MoE above -> softmax backward -> chain
+  // gating: d scores accumulated over every MoE above -> softmax backward -> chain.  With the weight
+  // gradients forked and an input-function branch, the gating's own group runs HERE after the branch has
+  // joined, on the branch's slab (free by then): forked, it queued behind the query encoder's group on the
+  // side stream and ended the step ~45 us later (configs[1] trace); its all-reduce keeps its place, last
+  const bool gate_here = br && !p->serial_wgrad();
   {
     ChainArgs a = chain_args(p, p->ch_gate, P);
     a.mode = CH_SOFTMAX; a.scores = p->P_("scores"); a.ldsc = (int)p->bufs["scores"].ld;
     a.dscore = p->P_("dscore");
     a.save = p->P_("gate_save"); a.save_layer_stride = P * D; a.save_chain_stride = NL * P * D;
     if (p->input_grads) { a.dX = p->P_("dxg"); a.lddx = p->bufs["dxg"].ld; a.dx_chain_stride = 0; }
-    GNOT_RUN(chain_bwd(a, p->k_gate(), P, p->wg_gate, "chain_bwd"));
+    if (gate_here) {
+      float* dz = p->P_(p->dz_name(p->k_gate()));
+      GNOT_RUN(guard_write(c, dz));
+      a.dz = dz; a.dz_layer_stride = P * D; a.dz_chain_stride = NL * P * D;
+      {
+        ProfScope ps(c, "chain_bwd", 2.0 * a.nchains * P * NL * (double)D * D);
+        GNOT_CK(launch_chain_bwd(cw_scratch(p, a, c.s), c.s));
+      }
+      GNOT_RUN(flush_deferred(c));           // the query encoder's group: side launch after this kernel
+    } else {
+      GNOT_RUN(chain_bwd(a, p->k_gate(), P, p->wg_gate, "chain_bwd"));
+    }
   }
   if (br) {                                // join the input-function branch
     hipEvent_t joinf = next_event(p);
     GNOT_CK(hipEventRecord(joinf, cf.s));
     GNOT_CK(hipStreamWaitEvent(c.s, joinf, 0));
+  }
+  if (gate_here && !p->wg_gate.jobs.empty()) {
+    {
+      ProfScope ps(c, "wgrad", group_flops(p->wg_gate));
+      GNOT_RUN(launch_group(p, p->wg_gate, p->P_("slab_wgrad2"), c.s));
+    }
+    if (p->grad_comm_on) {
+      hipEvent_t done = next_event(p);
+      GNOT_CK(hipEventRecord(done, c.s));
+      GNOT_RUN(grad_allreduce(p, p->wg_gate, done));
+    }
   }
   GNOT_RUN(flush_deferred(c));
   // join the side stream: every gradient is complete when the caller's stream moves on
