@@ -641,15 +641,17 @@ static void finish_group(gnot_plan* p, WgradGroup& G) {
   // d = 256: every job's whole 256 x 256 gradient in one workgroup (8 waves, 96 KiB LDS: one per CU).
   // The split-K target is fixed (r02bh: 192-512 all within noise), so the split counts the parity
   // tests exercise are the ones every run uses
-  // forked weight gradients (plans below kWgradSerialPoints) run beside the caller's stream: a group holding
-  // every CU's register file (the 256 x 256 kernel: 8 waves of 256 registers per CU) leaves the concurrent
-  // critical-path kernels no room, so forked groups take fewer workgroups.  Measured (round 6, interleaved
-  // sweeps `profiles/r06sw*`): configs[0] (d = 256) 128 of them in fp32 (9.54 -> 9.00 ms per step against
-  // 256), 64 in the bf16 mode (5.88 -> 5.47); configs[1] (the 128 x 128 kernel) 192 in fp32 (3.28 -> 3.21),
-  // 128 in the bf16 mode (the round-5 value)
-  const bool forked = !p->serial_wgrad();
-  const long wide_wgs = !forked ? 256 : p->npk() == 1 ? 64 : 128;
-  const long w128_wgs = forked && p->npk() != 1 ? 192 : kWide128Wgs;
+  // plans below kWgradSerialPoints fork their weight gradients beside the caller's stream (serial_wgrad): a
+  // group holding every CU's register file (the 256 x 256 kernel: 8 waves of 256 registers per CU) leaves the
+  // concurrent critical-path kernels no room, so such plans' groups take fewer workgroups.  Keyed on the plan
+  // size, not on the fork itself, so a plan gives bitwise the same gradients forked or serial
+  // (GNOT_WGRAD_OVERLAP, tests/test_gpu_recompute.py).  Measured (round 6, interleaved sweeps
+  // `profiles/r06sw*`): configs[0] (d = 256) 128 workgroups in fp32 (9.54 -> 9.00 ms per step against 256),
+  // 64 in the bf16 mode (5.88 -> 5.47); configs[1] (the 128 x 128 kernel) 192 in fp32 (3.28 -> 3.21), 128 in
+  // the bf16 mode (the round-5 value)
+  const bool small = p->P < gnot_plan::kWgradSerialPoints;
+  const long wide_wgs = !small ? 256 : p->npk() == 1 ? 64 : 128;
+  const long w128_wgs = small && p->npk() != 1 ? 192 : kWide128Wgs;
   G.wide = G.x6 && p->D == 256 && !G.jobs.empty();
   for (const auto& J : G.jobs)
     if (J.out > 256 || J.in > 256) G.wide = false;
